@@ -1,0 +1,37 @@
+# Builds the gfx950 HIP C-ABI library in-tree (travels to the GPU box with the
+# snapshot) and the oracle's C helpers.  Usage: make -j8
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := image_processor_pipeline_amd
+CSRC := $(PKG)/csrc
+SRCS := $(CSRC)/ipp_gather.hip $(CSRC)/ipp_hsv.hip $(CSRC)/ipp_resample.hip $(CSRC)/ipp_pipe.hip \
+        $(CSRC)/ipp_ccl.hip
+HOST_SRCS := $(CSRC)/ipp_host.cpp
+HDRS := include/ipp.h $(CSRC)/ipp_device.h $(CSRC)/ipp_hsv.h
+OBJDIR := build/obj
+OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS)) $(OBJDIR)/ipp_host.o
+LIB := $(PKG)/libipp.so
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-function
+HOSTFLAGS := -O2 -std=c++17 -fPIC -Iinclude
+
+all: $(LIB)
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS) | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/ipp_host.o: $(CSRC)/ipp_host.cpp $(HDRS) | $(OBJDIR)
+	g++ $(HOSTFLAGS) -c $< -o $@
+
+$(OBJDIR):
+	mkdir -p $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread
+
+asm: | $(OBJDIR)
+	for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) -S --cuda-device-only $$f -o $(OBJDIR)/$$(basename $$f .hip).s; done
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean asm

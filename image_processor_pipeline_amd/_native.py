@@ -1,0 +1,125 @@
+"""ctypes binding of the gfx950 C-ABI library ``libipp.so`` (include/ipp.h).
+
+The library is built in-tree (``make`` / ``__graft_entry__.build()``).  There
+is NO CPU fallback: if the library or a GPU is missing, the device ops raise
+``NativeUnavailable`` loudly instead of computing anything elsewhere.
+
+NumPy structured dtypes below mirror the C structs field for field (offsets
+are checked against the C compiler in tests/test_abi.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "libipp.so"
+
+IPP_OK = 0
+IPP_E_ARG = -1
+IPP_E_LAUNCH = -2
+IPP_E_RANGE = -3
+IPP_MAX_HSV_RANGES = 16
+IPP_RS_PREMULTIPLY = 1
+IPP_RS_UNPREMULTIPLY = 2
+
+
+class NativeUnavailable(RuntimeError):
+    """The HIP C-ABI library could not be loaded (never silently bypassed)."""
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_I4 = np.int32
+_I8 = np.int64
+
+GATHER_DESC = np.dtype([
+    ("src_off", _I8), ("dst_off", _I8), ("src_pitch", _I4), ("src_cn", _I4),
+    ("src_w", _I4), ("src_h", _I4), ("in_x0", _I4), ("in_y0", _I4), ("in_w", _I4), ("in_h", _I4),
+    ("a0", _I4), ("a1", _I4), ("a2", _I4), ("a3", _I4), ("a4", _I4), ("a5", _I4),
+    ("out_w", _I4), ("out_h", _I4), ("off_x", _I4), ("off_y", _I4), ("flip", _I4), ("dst_pitch", _I4),
+], align=True)
+
+COPY_DESC = np.dtype([
+    ("src_off", _I8), ("dst_off", _I8), ("src_pitch", _I4), ("dst_pitch", _I4),
+    ("x0", _I4), ("y0", _I4), ("w", _I4), ("h", _I4), ("cn", _I4), ("flip", _I4),
+], align=True)
+
+HSV_RANGE = np.dtype([("lo", _I4, (3,)), ("hi", _I4, (3,)), ("zone", _I4, (4,))], align=True)
+HSV_PARAMS = np.dtype([("n_ranges", _I4), ("bgr", _I4), ("r", HSV_RANGE, (IPP_MAX_HSV_RANGES,))], align=True)
+
+IMAGE_DESC = np.dtype([("off", _I8), ("w", _I4), ("h", _I4), ("pitch", _I4), ("cn", _I4)], align=True)
+
+RESAMPLE_DESC = np.dtype([
+    ("src_off", _I8), ("dst_off", _I8), ("src_pitch", _I4), ("dst_pitch", _I4),
+    ("in_len", _I4), ("out_len", _I4), ("lines", _I4), ("line0", _I4), ("ksize", _I4), ("pad_", _I4),
+    ("coef_off", _I8),
+], align=True)
+
+PASTE_DESC = np.dtype([
+    ("bg_off", _I8), ("ov_off", _I8), ("dst_off", _I8),
+    ("bg_w", _I4), ("bg_h", _I4), ("bg_pitch", _I4), ("dst_pitch", _I4),
+    ("ov_w", _I4), ("ov_h", _I4), ("ov_pitch", _I4), ("x", _I4), ("y", _I4), ("pad_", _I4),
+], align=True)
+
+PIPE_DESC = np.dtype([("g", GATHER_DESC), ("h", RESAMPLE_DESC), ("v", RESAMPLE_DESC), ("p", PASTE_DESC)],
+                     align=True)
+
+# (symbol, restype, argtypes) — every entry point declared in include/ipp.h.
+_P = ctypes.c_void_p
+_I = ctypes.c_int32
+_L = ctypes.c_int64
+_D = ctypes.c_double
+SIGNATURES = {
+    "ipp_rotate_flip_nearest": (_I, [_P, _P, _P, _I, _I, _I, _P]),
+    "ipp_copy_window": (_I, [_P, _P, _P, _I, _I, _I, _P]),
+    "ipp_hsv_mask": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "ipp_lanczos_h": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "ipp_lanczos_v": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "ipp_paste_blend": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
+    "ipp_pipe_hpass": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "ipp_pipe_vblend": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "ipp_ccl_keep_largest": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "ipp_alpha_bbox": (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    "ipp_plan_lanczos": (_L, [_I, _D, _D, _I, _P, _L]),
+    "ipp_plan_lanczos_ksize": (_I, [_D, _D, _I]),
+    "ipp_plan_lanczos_batch": (_I, [_I, _P, _P, _P, _P, _L, _I]),
+    "ipp_plan_opaque_bbox": (_I, [_I, _I, _P, _I, _I, _P]),
+    "ipp_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libipp.so once; raise NativeUnavailable if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise NativeUnavailable(
+            f"{LIB_PATH} not found — build it with `make` or __graft_entry__.build(); "
+            "there is no CPU fallback for the hot path")
+    try:
+        lib = ctypes.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | getattr(os, "RTLD_LOCAL", 0))
+    except OSError as e:  # pragma: no cover - environment dependent
+        raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != IPP_OK:
+        raise NativeError(f"{what} failed with code {rc}")
+
+
+def np_ptr(a: np.ndarray) -> int:
+    return a.ctypes.data

@@ -1,0 +1,94 @@
+// ipp_device.h — device helpers shared by the gfx950 kernels.
+//
+// Pixels travel packed little-endian in one dword: byte 0 = channel 0 at the
+// lowest address (R for Pillow-order images, B for cv2-order images), byte 3 =
+// alpha.  All arithmetic is integer and reproduces the library code the
+// reference calls bit-for-bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ipp.h"
+
+#define IPP_CHECK_LAUNCH()                                  \
+    do {                                                    \
+        if (hipGetLastError() != hipSuccess) return IPP_E_LAUNCH; \
+    } while (0)
+
+// A dword load from a byte address with no alignment promise.  gfx950 runs the
+// HSA queues in unaligned-access mode, so global_load_dword needs no 4-byte
+// alignment; the caller guarantees the 4 bytes are inside the allocation.
+typedef uint32_t __attribute__((aligned(1), may_alias)) ipp_u32_unaligned;
+
+__device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* p) {
+    return *reinterpret_cast<const ipp_u32_unaligned*>(p);
+}
+
+// RGB (3 bytes at p) → packed RGBA with alpha 255 (Pillow convert('RGBA'),
+// rotations.py:55).  `wide_ok` says a 4-byte read at p stays inside the image.
+__device__ __forceinline__ uint32_t load_rgb_opaque(const uint8_t* p, bool wide_ok) {
+    if (wide_ok) return ld_u32_unaligned(p) | 0xFF000000u;
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | 0xFF000000u;
+}
+
+// MULDIV255 / DIV255 of libImaging (Convert.c, Paste.c):
+//   DIV255(v) = ((v + 128) + ((v + 128) >> 8)) >> 8
+__device__ __forceinline__ uint32_t div255(uint32_t v) {
+    v += 128u;
+    return (v + (v >> 8)) >> 8;
+}
+
+// Convert.c rgbA2rgba: c' = MULDIV255(c, a) for the three colour bytes.
+__device__ __forceinline__ uint32_t premultiply(uint32_t px) {
+    uint32_t a = px >> 24;
+    if (a == 255u) return px;
+    if (a == 0u) return 0u;
+    uint32_t c0 = div255((px & 0xFFu) * a);
+    uint32_t c1 = div255(((px >> 8) & 0xFFu) * a);
+    uint32_t c2 = div255(((px >> 16) & 0xFFu) * a);
+    return c0 | (c1 << 8) | (c2 << 16) | (a << 24);
+}
+
+// Convert.c rgba2rgbA: alpha 0 or 255 → unchanged, else min(255, 255*c / a)
+// (integer division).  The float quotient is corrected by ±1 so the result is
+// the exact floor whatever the division's rounding.
+__device__ __forceinline__ uint32_t unpremultiply(uint32_t px) {
+    uint32_t a = px >> 24;
+    if (a == 255u || a == 0u) return px;
+    float ra = __builtin_amdgcn_rcpf((float)a);
+    uint32_t out = a << 24;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        uint32_t n = 255u * ((px >> (8 * c)) & 0xFFu);
+        uint32_t q = (uint32_t)((float)n * ra);
+        if ((q + 1u) * a <= n) ++q;
+        if (q * a > n) --q;
+        out |= (q > 255u ? 255u : q) << (8 * c);
+    }
+    return out;
+}
+
+// Resample.c clip8: clamp(ss >> 22, 0, 255) with an arithmetic shift.
+__device__ __forceinline__ uint32_t clip8(int32_t ss) {
+    int32_t v = ss >> 22;
+    return (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+// Python slice(start, stop).indices(length) for step 1 (zone masks,
+// filtres_liste.py:102-103: mask[t : H-b, l : W-r] = 255).
+__device__ __forceinline__ void slice_indices(int start, int stop, int length, int& lo, int& hi) {
+    if (start < 0) { start += length; if (start < 0) start = 0; } else if (start > length) start = length;
+    if (stop < 0) { stop += length; if (stop < 0) stop = 0; } else if (stop > length) stop = length;
+    lo = start;
+    hi = stop < start ? start : stop;
+}
+
+// XCD-aware block remap (cdna_hip_programming.md §5.5 T1): the dispatcher deals
+// linear block ids round-robin over the 8 XCDs; remap so that consecutive
+// logical tiles (the tiles of one image) share an XCD and its L2.  Bijective
+// for any count.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nblocks) {
+    uint32_t xcd = b & 7u, slot = b >> 3;
+    uint32_t q = nblocks >> 3, r = nblocks & 7u;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}

@@ -1,0 +1,202 @@
+// ipp_gather.hip — K1..K5: margin crop → RGBA → NEAREST rotate (expand) →
+// alpha-bbox crop → flip, as ONE gather per output pixel; plus the plain
+// window copy/flip and the alpha bounding-box reduction.
+//
+// Reference call sites: recadrages.py:46 (slice), rotations.py:55 (convert
+// RGBA), :96 (rotate, NEAREST, expand), :99-101 (getbbox/crop),
+// symmetry.py:114-119 (cv2.flip 1/0/-1), pixels_isolés.py:77-81 (crop-fit).
+// Library arithmetic reproduced: Pillow Geometry.c affine_fixed (16.16 int32
+// accumulation, arithmetic >> 16, out-of-range → zero pixel).
+//
+// Layout: each thread owns 4 horizontally adjacent output pixels (16 bytes of
+// RGBA) so a wave stores 1 KiB with dwordx4 stores; a 256-thread block covers a
+// 64×16 output tile.  Blocks are remapped so the tiles of one image share an
+// XCD (its source stays in that XCD's L2).
+#include "ipp_device.h"
+
+namespace {
+
+constexpr int TILE_W = 64, TILE_H = 16, PX_PER_THREAD = 4;
+
+struct TileGrid {
+    int tiles_x, tiles_y;
+};
+
+__device__ __forceinline__ uint32_t gather_pixel(const uint8_t* __restrict__ src, const ipp_gather_desc& d,
+                                                 uint32_t rowx, uint32_t rowy, int X) {
+    int32_t xx = (int32_t)(rowx + (uint32_t)X * (uint32_t)d.a0);
+    int32_t yy = (int32_t)(rowy + (uint32_t)X * (uint32_t)d.a3);
+    int xin = xx >> 16, yin = yy >> 16;
+    if ((unsigned)xin >= (unsigned)d.in_w || (unsigned)yin >= (unsigned)d.in_h) return 0u;
+    int sx = d.in_x0 + xin, sy = d.in_y0 + yin;
+    const uint8_t* p = src + d.src_off + (int64_t)sy * d.src_pitch;
+    if (d.src_cn == 4) return *reinterpret_cast<const uint32_t*>(p + 4 * sx);
+    bool wide_ok = (sy < d.src_h - 1) || (sx < d.src_w - 1);
+    return load_rgb_opaque(p + 3 * sx, wide_ok);
+}
+
+__global__ void __launch_bounds__(256)
+k_rotate_flip_nearest(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                      const ipp_gather_desc* __restrict__ descs, int tiles_x, int tiles_y) {
+    const uint32_t nblk = gridDim.x;
+    const uint32_t b = xcd_remap(blockIdx.x, nblk);
+    const int per_img = tiles_x * tiles_y;
+    const int img = b / per_img;
+    const int t = b - img * per_img;
+    const int ty = t / tiles_x, tx = t - ty * tiles_x;
+    const ipp_gather_desc d = descs[img];
+    const int y = ty * TILE_H + (int)(threadIdx.x >> 4);
+    const int x0 = tx * TILE_W + (int)(threadIdx.x & 15) * PX_PER_THREAD;
+    if (y >= d.out_h || x0 >= d.out_w) return;
+
+    const int fy = (d.flip & 2) ? d.out_h - 1 - y : y;
+    const int Y = d.off_y + fy;
+    const uint32_t rowx = (uint32_t)d.a2 + (uint32_t)Y * (uint32_t)d.a1;
+    const uint32_t rowy = (uint32_t)d.a5 + (uint32_t)Y * (uint32_t)d.a4;
+    uint32_t px[PX_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < PX_PER_THREAD; ++k) {
+        const int x = x0 + k;
+        const int fx = (d.flip & 1) ? d.out_w - 1 - x : x;
+        px[k] = (x < d.out_w) ? gather_pixel(src, d, rowx, rowy, d.off_x + fx) : 0u;
+    }
+    uint8_t* o = dst + d.dst_off + (int64_t)y * d.dst_pitch + 4 * x0;
+    const bool full = (x0 + PX_PER_THREAD <= d.out_w);
+    if (full && ((reinterpret_cast<uintptr_t>(o) & 15u) == 0)) {
+        *reinterpret_cast<uint4*>(o) = make_uint4(px[0], px[1], px[2], px[3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < PX_PER_THREAD; ++k)
+            if (x0 + k < d.out_w) reinterpret_cast<uint32_t*>(o)[k] = px[k];
+    }
+}
+
+// Window copy with optional mirror, any bytes-per-pixel (1..4).
+__global__ void __launch_bounds__(256)
+k_copy_window(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+              const ipp_copy_desc* __restrict__ descs, int tiles_x, int tiles_y) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int per_img = tiles_x * tiles_y;
+    const int img = b / per_img;
+    const int t = b - img * per_img;
+    const int ty = t / tiles_x, tx = t - ty * tiles_x;
+    const ipp_copy_desc d = descs[img];
+    const int y = ty * TILE_H + (int)(threadIdx.x >> 4);
+    const int x0 = tx * TILE_W + (int)(threadIdx.x & 15) * PX_PER_THREAD;
+    if (y >= d.h || x0 >= d.w) return;
+    const int sy = d.y0 + ((d.flip & 2) ? d.h - 1 - y : y);
+    const uint8_t* s = src + d.src_off + (int64_t)sy * d.src_pitch;
+    uint8_t* o = dst + d.dst_off + (int64_t)y * d.dst_pitch;
+    for (int k = 0; k < PX_PER_THREAD; ++k) {
+        const int x = x0 + k;
+        if (x >= d.w) break;
+        const int sx = d.x0 + ((d.flip & 1) ? d.w - 1 - x : x);
+        const uint8_t* sp = s + (int64_t)sx * d.cn;
+        uint8_t* op = o + (int64_t)x * d.cn;
+        for (int c = 0; c < d.cn; ++c) op[c] = sp[c];
+    }
+}
+
+// Alpha bbox: per block min/max over its tile with wave reductions, then four
+// device-scope atomics.  bbox must be pre-set to (INT_MAX, INT_MAX, -1, -1).
+__global__ void __launch_bounds__(256)
+k_alpha_bbox(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
+             int tiles_x, int tiles_y, int32_t* __restrict__ bbox) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int per_img = tiles_x * tiles_y;
+    const int im = b / per_img;
+    const int t = b - im * per_img;
+    const int ty = t / tiles_x, tx = t - ty * tiles_x;
+    const ipp_image_desc d = descs[im];
+    const int y = ty * TILE_H + (int)(threadIdx.x >> 4);
+    const int x0 = tx * TILE_W + (int)(threadIdx.x & 15) * PX_PER_THREAD;
+    int xmin = INT32_MAX, ymin = INT32_MAX, xmax = -1, ymax = -1;
+    if (y < d.h) {
+        const uint8_t* row = img + d.off + (int64_t)y * d.pitch;
+        for (int k = 0; k < PX_PER_THREAD; ++k) {
+            const int x = x0 + k;
+            if (x < d.w && row[(int64_t)x * d.cn + (d.cn - 1)] != 0) {
+                xmin = min(xmin, x);
+                xmax = max(xmax, x);
+                ymin = min(ymin, y);
+                ymax = max(ymax, y);
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        xmin = min(xmin, __shfl_xor(xmin, off));
+        ymin = min(ymin, __shfl_xor(ymin, off));
+        xmax = max(xmax, __shfl_xor(xmax, off));
+        ymax = max(ymax, __shfl_xor(ymax, off));
+    }
+    if ((threadIdx.x & 63) == 0 && xmax >= 0) {
+        atomicMin(&bbox[4 * im + 0], xmin);
+        atomicMin(&bbox[4 * im + 1], ymin);
+        atomicMax(&bbox[4 * im + 2], xmax + 1);
+        atomicMax(&bbox[4 * im + 3], ymax + 1);
+    }
+}
+
+__global__ void k_bbox_init(int32_t* bbox, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        bbox[4 * i + 0] = INT32_MAX;
+        bbox[4 * i + 1] = INT32_MAX;
+        bbox[4 * i + 2] = -1;
+        bbox[4 * i + 3] = -1;
+    }
+}
+
+__global__ void k_bbox_finish(int32_t* bbox, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && bbox[4 * i + 2] < 0) {
+        bbox[4 * i + 0] = bbox[4 * i + 1] = -1;
+    }
+}
+
+inline bool grid_ok(int64_t blocks) { return blocks > 0 && blocks < (int64_t)INT32_MAX; }
+
+}  // namespace
+
+extern "C" int ipp_rotate_flip_nearest(const uint8_t* src, uint8_t* dst, const ipp_gather_desc* descs,
+                                       int32_t n_images, int32_t max_out_w, int32_t max_out_h,
+                                       void* stream) {
+    if (n_images == 0) return IPP_OK;
+    if (!src || !dst || !descs || n_images < 0 || max_out_w <= 0 || max_out_h <= 0) return IPP_E_ARG;
+    const int tx = (max_out_w + TILE_W - 1) / TILE_W, ty = (max_out_h + TILE_H - 1) / TILE_H;
+    const int64_t blocks = (int64_t)tx * ty * n_images;
+    if (!grid_ok(blocks)) return IPP_E_ARG;
+    hipLaunchKernelGGL(k_rotate_flip_nearest, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
+                       src, dst, descs, tx, ty);
+    IPP_CHECK_LAUNCH();
+    return IPP_OK;
+}
+
+extern "C" int ipp_copy_window(const uint8_t* src, uint8_t* dst, const ipp_copy_desc* descs, int32_t n_images,
+                               int32_t max_w, int32_t max_h, void* stream) {
+    if (n_images == 0) return IPP_OK;
+    if (!src || !dst || !descs || n_images < 0 || max_w <= 0 || max_h <= 0) return IPP_E_ARG;
+    const int tx = (max_w + TILE_W - 1) / TILE_W, ty = (max_h + TILE_H - 1) / TILE_H;
+    const int64_t blocks = (int64_t)tx * ty * n_images;
+    if (!grid_ok(blocks)) return IPP_E_ARG;
+    hipLaunchKernelGGL(k_copy_window, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, src, dst, descs,
+                       tx, ty);
+    IPP_CHECK_LAUNCH();
+    return IPP_OK;
+}
+
+extern "C" int ipp_alpha_bbox(const uint8_t* img, const ipp_image_desc* descs, int32_t n_images, int32_t max_w,
+                              int32_t max_h, int32_t* bbox, void* stream) {
+    if (n_images == 0) return IPP_OK;
+    if (!img || !descs || !bbox || n_images < 0 || max_w <= 0 || max_h <= 0) return IPP_E_ARG;
+    const int tx = (max_w + TILE_W - 1) / TILE_W, ty = (max_h + TILE_H - 1) / TILE_H;
+    const int64_t blocks = (int64_t)tx * ty * n_images;
+    if (!grid_ok(blocks)) return IPP_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = (n_images + 255) / 256;
+    hipLaunchKernelGGL(k_bbox_init, dim3(nb), dim3(256), 0, s, bbox, n_images);
+    hipLaunchKernelGGL(k_alpha_bbox, dim3((uint32_t)blocks), dim3(256), 0, s, img, descs, tx, ty, bbox);
+    hipLaunchKernelGGL(k_bbox_finish, dim3(nb), dim3(256), 0, s, bbox, n_images);
+    IPP_CHECK_LAUNCH();
+    return IPP_OK;
+}

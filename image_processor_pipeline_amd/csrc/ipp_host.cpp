@@ -1,0 +1,175 @@
+// ipp_host.cpp — host-side planning for the hot path (CPU, C ABI).
+//
+// These functions reproduce the HOST arithmetic of the libraries the
+// reference calls, so the device kernels receive the exact integers Pillow
+// would use:
+//   * ipp_plan_lanczos: Pillow Resample.c precompute_coeffs +
+//     normalize_coeffs_8bpc for the LANCZOS filter (support 3, sinc·sinc/3,
+//     double precision, the same libm sin()), PRECISION_BITS = 22 — the taps
+//     behind overlays.py:129.
+//   * ipp_plan_opaque_bbox: the getbbox() of rotations.py:99 for an opaque
+//     source, solved per canvas row from the 16.16 affine map with exact
+//     integer inequalities (no canvas is materialised).
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+#include "ipp.h"
+
+namespace {
+
+inline double sinc_filter(double x) {
+    if (x == 0.0) return 1.0;
+    x = x * M_PI;
+    return sin(x) / x;
+}
+
+inline double lanczos_filter(double x) {
+    if (-3.0 <= x && x < 3.0) return sinc_filter(x) * sinc_filter(x / 3);
+    return 0.0;
+}
+
+inline int ksize_of(double in0, double in1, int out_size) {
+    const double scale = (double)((float)in1 - (float)in0) / out_size;
+    const double filterscale = scale < 1.0 ? 1.0 : scale;
+    const double support = 3.0 * filterscale;
+    return (int)ceil(support) * 2 + 1;
+}
+
+// floor(a / b) and ceil(a / b) for b != 0 (int64).
+inline int64_t floordiv(int64_t a, int64_t b) {
+    int64_t q = a / b, r = a % b;
+    return (r != 0 && ((r < 0) != (b < 0))) ? q - 1 : q;
+}
+inline int64_t ceildiv(int64_t a, int64_t b) { return -floordiv(-a, b); }
+
+// X range where lo <= c + X*a <= hi (inclusive); returns false if empty.
+inline bool solve_range(int64_t c, int64_t a, int64_t lo, int64_t hi, int64_t& xlo, int64_t& xhi) {
+    if (a == 0) {
+        if (c < lo || c > hi) return false;
+        xlo = INT64_MIN / 4;
+        xhi = INT64_MAX / 4;
+        return true;
+    }
+    if (a > 0) {
+        xlo = ceildiv(lo - c, a);
+        xhi = floordiv(hi - c, a);
+    } else {
+        xlo = ceildiv(hi - c, a);
+        xhi = floordiv(lo - c, a);
+    }
+    return xlo <= xhi;
+}
+
+}  // namespace
+
+extern "C" int32_t ipp_plan_lanczos_ksize(double in0, double in1, int32_t out_size) {
+    if (out_size <= 0) return IPP_E_ARG;
+    return ksize_of(in0, in1, out_size);
+}
+
+extern "C" int64_t ipp_plan_lanczos(int32_t in_size, double in0, double in1, int32_t out_size, int32_t* out,
+                                    int64_t out_capacity) {
+    if (in_size <= 0 || out_size <= 0) return IPP_E_ARG;
+    const float fin0 = (float)in0, fin1 = (float)in1;  // Resample.c takes float box[4]
+    const double scale = (double)(fin1 - fin0) / out_size;
+    const double filterscale = scale < 1.0 ? 1.0 : scale;
+    const double support = 3.0 * filterscale;
+    const int ksize = (int)ceil(support) * 2 + 1;
+    const int64_t need = 2 * (int64_t)out_size + (int64_t)out_size * ksize;
+    if (out == nullptr) return -need;
+    if (out_capacity < need) return IPP_E_ARG;
+    int32_t* bounds = out;
+    int32_t* kk = out + 2 * (int64_t)out_size;
+    std::vector<double> k(ksize);
+    const double ss = 1.0 / filterscale;
+    for (int xx = 0; xx < out_size; ++xx) {
+        const double center = fin0 + (xx + 0.5) * scale;
+        double ww = 0.0;
+        int xmin = (int)(center - support + 0.5);
+        if (xmin < 0) xmin = 0;
+        int xmax = (int)(center + support + 0.5);
+        if (xmax > in_size) xmax = in_size;
+        xmax -= xmin;
+        for (int x = 0; x < xmax; ++x) {
+            const double w = lanczos_filter((x + xmin - center + 0.5) * ss);
+            k[x] = w;
+            ww += w;
+        }
+        for (int x = 0; x < xmax; ++x)
+            if (ww != 0.0) k[x] /= ww;
+        int32_t* kq = kk + (int64_t)xx * ksize;
+        for (int x = 0; x < ksize; ++x) {
+            const double v = x < xmax ? k[x] : 0.0;
+            kq[x] = v < 0 ? (int32_t)(-0.5 + v * (1 << 22)) : (int32_t)(0.5 + v * (1 << 22));
+        }
+        bounds[2 * xx] = xmin;
+        bounds[2 * xx + 1] = xmax;
+    }
+    return ksize;
+}
+
+// Batch planner: n independent axes, written at int32 offsets; threads split
+// the list.  Returns 0 or the first error.
+extern "C" int ipp_plan_lanczos_batch(int32_t n, const int32_t* in_sizes, const int32_t* out_sizes,
+                                      const int64_t* offsets, int32_t* out, int64_t out_capacity,
+                                      int32_t n_threads) {
+    if (n < 0 || (n > 0 && (!in_sizes || !out_sizes || !offsets || !out))) return IPP_E_ARG;
+    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min(nt, 64));
+    std::vector<int> err(nt, 0);
+    auto work = [&](int t) {
+        for (int i = t; i < n; i += nt) {
+            const int64_t r = ipp_plan_lanczos(in_sizes[i], 0.0, (double)in_sizes[i], out_sizes[i], out + offsets[i],
+                                               out_capacity - offsets[i]);
+            if (r < 0) err[t] = (int)r;
+        }
+    };
+    if (nt == 1 || n < 64) {
+        nt = 1;
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
+        for (auto& x : th) x.join();
+    }
+    for (int e : err)
+        if (e) return e;
+    return IPP_OK;
+}
+
+extern "C" int ipp_plan_opaque_bbox(int32_t in_w, int32_t in_h, const int32_t a[6], int32_t nw, int32_t nh,
+                                    int32_t bbox[4]) {
+    if (in_w <= 0 || in_h <= 0 || nw <= 0 || nh <= 0 || !a || !bbox) return IPP_E_ARG;
+    int64_t x0 = INT64_MAX, x1 = -1, y0 = INT64_MAX, y1 = -1;
+    const int64_t ux = (int64_t)in_w * 65536 - 1, uy = (int64_t)in_h * 65536 - 1;
+    for (int64_t Y = 0; Y < nh; ++Y) {
+        const int64_t cx = (int64_t)a[2] + Y * a[1];
+        const int64_t cy = (int64_t)a[5] + Y * a[4];
+        int64_t lo1, hi1, lo2, hi2;
+        if (!solve_range(cx, a[0], 0, ux, lo1, hi1)) continue;
+        if (!solve_range(cy, a[3], 0, uy, lo2, hi2)) continue;
+        const int64_t lo = std::max<int64_t>(std::max(lo1, lo2), 0);
+        const int64_t hi = std::min<int64_t>(std::min(hi1, hi2), nw - 1);
+        if (lo > hi) continue;
+        x0 = std::min(x0, lo);
+        x1 = std::max(x1, hi);
+        y0 = std::min(y0, Y);
+        y1 = std::max(y1, Y);
+    }
+    if (x1 < 0) {
+        bbox[0] = bbox[1] = bbox[2] = bbox[3] = -1;
+    } else {
+        bbox[0] = (int32_t)x0;
+        bbox[1] = (int32_t)y0;
+        bbox[2] = (int32_t)x1 + 1;
+        bbox[3] = (int32_t)y1 + 1;
+    }
+    return IPP_OK;
+}
+
+extern "C" const char* ipp_version(void) { return "ipp 0.1.0 (gfx950)"; }

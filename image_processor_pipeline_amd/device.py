@@ -1,0 +1,275 @@
+"""Tensor-level device ops: thin wrappers that plan on the host and launch the
+gfx950 kernels of libipp.so on torch's current HIP stream.
+
+Tensors are HWC ``torch.uint8`` on a ROCm device.  Every op calls the HIP
+C-ABI; if the library (or the GPU) is missing the call raises — there is no
+CPU fallback in the product path.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import geometry as G
+
+SYM_FLIP = {"o": 0, "h": 1, "v": 2, "hv": 3}
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _to_dev(a: np.ndarray, device) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(device)
+
+
+def _require_cuda(t: torch.Tensor, name: str) -> None:
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.uint8):
+        raise N.NativeUnavailable(f"{name}: expected a uint8 tensor on a ROCm device (no CPU fallback)")
+
+
+# ---------------------------------------------------------------------------
+# Rotate (+ margin crop, bbox crop, flip): rotations.py / recadrages.py /
+# symmetry.py in one gather.
+# ---------------------------------------------------------------------------
+
+@dataclass
+class GatherPlan:
+    descs: np.ndarray              # GATHER_DESC[n]
+    shapes: List[Tuple[int, int]]  # output (h, w) per image
+    offsets: np.ndarray            # byte offset per output (packed, 16-B aligned rows)
+    pitches: np.ndarray
+    total_bytes: int
+    max_w: int
+    max_h: int
+
+
+def plan_rotate_flip(src_dims: Sequence[Tuple[int, int, int]], angles: Sequence[float],
+                     flips: Sequence[int], windows: Optional[Sequence[Tuple[int, int, int, int]]] = None,
+                     src_offsets: Optional[Sequence[int]] = None, src_pitches: Optional[Sequence[int]] = None,
+                     crop_to_bbox: bool = True) -> GatherPlan:
+    """Plan the fused gather for opaque (3-channel) or alpha-free sources.
+
+    src_dims: (h, w, cn) per source; windows: (x0, y0, w, h) crop window per
+    source (default: whole image).  The rotated canvas is cropped to its
+    alpha bbox analytically (opaque input ⇒ exact; rotations.py:99-109)."""
+    n = len(src_dims)
+    d = np.zeros(n, N.GATHER_DESC)
+    shapes, offs, pitches = [], np.zeros(n, np.int64), np.zeros(n, np.int64)
+    off = 0
+    max_w = max_h = 1
+    for i, (h, w, cn) in enumerate(src_dims):
+        x0, y0, iw, ih = windows[i] if windows is not None else (0, 0, w, h)
+        plan = G.rotation_plan(iw, ih, float(angles[i]))
+        ox, oy, ow, oh = 0, 0, plan.nw, plan.nh
+        if crop_to_bbox:
+            bb = G.rotated_bbox(iw, ih, plan)
+            if bb is not None and bb[2] > bb[0] and bb[3] > bb[1]:
+                ox, oy, ow, oh = bb[0], bb[1], bb[2] - bb[0], bb[3] - bb[1]
+        pitch = (4 * ow + 15) // 16 * 16
+        d[i]["src_off"] = src_offsets[i] if src_offsets is not None else 0
+        d[i]["src_pitch"] = src_pitches[i] if src_pitches is not None else w * cn
+        d[i]["src_cn"] = cn
+        d[i]["src_w"], d[i]["src_h"] = w, h
+        d[i]["in_x0"], d[i]["in_y0"], d[i]["in_w"], d[i]["in_h"] = x0, y0, iw, ih
+        for k in range(6):
+            d[i][f"a{k}"] = plan.A[k]
+        d[i]["out_w"], d[i]["out_h"] = ow, oh
+        d[i]["off_x"], d[i]["off_y"] = ox, oy
+        d[i]["flip"] = int(flips[i])
+        d[i]["dst_off"] = off
+        d[i]["dst_pitch"] = pitch
+        shapes.append((oh, ow))
+        offs[i] = off
+        pitches[i] = pitch
+        off += pitch * oh
+        max_w, max_h = max(max_w, ow), max(max_h, oh)
+    return GatherPlan(d, shapes, offs, pitches, off, max_w, max_h)
+
+
+def rotate_flip_nearest(src: torch.Tensor, plan: GatherPlan, out: Optional[torch.Tensor] = None,
+                        descs_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Launch the gather over a flat source buffer; returns the packed output."""
+    _require_cuda(src, "rotate_flip_nearest")
+    lib = N.load()
+    if out is None:
+        out = torch.empty(max(plan.total_bytes, 16), dtype=torch.uint8, device=src.device)
+    if descs_dev is None:
+        descs_dev = _to_dev(plan.descs, src.device)
+    N.check(lib.ipp_rotate_flip_nearest(src.data_ptr(), out.data_ptr(), descs_dev.data_ptr(), len(plan.descs),
+                                        plan.max_w, plan.max_h, _stream(src.device)), "ipp_rotate_flip_nearest")
+    return out
+
+
+def unpack(buf: torch.Tensor, plan: GatherPlan, cn: int = 4) -> List[torch.Tensor]:
+    """Views (h, w, cn) into a packed pitched buffer."""
+    outs = []
+    for (h, w), off, pitch in zip(plan.shapes, plan.offsets, plan.pitches):
+        outs.append(torch.as_strided(buf, (h, w, cn), (int(pitch), cn, 1), int(off)))
+    return outs
+
+
+def rotate_crop_single(img: torch.Tensor, angle: float, flip: int = 0) -> torch.Tensor:
+    """rotations.py:55,96-109 for one image (3- or 4-channel, HWC).
+
+    Opaque sources use the analytic bbox; sources with an alpha channel are
+    rotated onto the full canvas, their alpha bbox is reduced on the device
+    and the window copied out (Pillow semantics incl. the None/empty-bbox
+    fallback to the uncropped canvas)."""
+    _require_cuda(img, "rotate_crop_single")
+    img = img.contiguous()
+    h, w, cn = img.shape
+    if cn == 3:
+        plan = plan_rotate_flip([(h, w, 3)], [angle], [flip])
+        buf = rotate_flip_nearest(img.reshape(-1), plan)
+        return unpack(buf, plan)[0].contiguous()
+    plan = plan_rotate_flip([(h, w, 4)], [angle], [0], crop_to_bbox=False)
+    canvas = unpack(rotate_flip_nearest(img.reshape(-1), plan), plan)[0].contiguous()
+    bb = alpha_bbox([canvas])[0]
+    if bb is None or bb[2] <= bb[0] or bb[3] <= bb[1]:
+        x0, y0, x1, y1 = 0, 0, canvas.shape[1], canvas.shape[0]
+    else:
+        x0, y0, x1, y1 = bb
+    return copy_window(canvas, (x0, y0, x1 - x0, y1 - y0), flip)
+
+
+# ---------------------------------------------------------------------------
+# Window copy / flip (recadrages.py:46, crop_square.py:196, symmetry.py:114-119)
+# ---------------------------------------------------------------------------
+
+def copy_window(img: torch.Tensor, window: Optional[Tuple[int, int, int, int]] = None,
+                flip: int = 0) -> torch.Tensor:
+    _require_cuda(img, "copy_window")
+    img = img.contiguous()
+    h, w, cn = img.shape
+    x0, y0, ww, wh = window if window is not None else (0, 0, w, h)
+    out = torch.empty((wh, ww, cn), dtype=torch.uint8, device=img.device)
+    if ww == 0 or wh == 0:
+        return out
+    d = np.zeros(1, N.COPY_DESC)
+    d[0]["src_pitch"], d[0]["dst_pitch"] = w * cn, ww * cn
+    d[0]["x0"], d[0]["y0"], d[0]["w"], d[0]["h"], d[0]["cn"], d[0]["flip"] = x0, y0, ww, wh, cn, flip
+    dd = _to_dev(d, img.device)
+    N.check(N.load().ipp_copy_window(img.data_ptr(), out.data_ptr(), dd.data_ptr(), 1, ww, wh,
+                                     _stream(img.device)), "ipp_copy_window")
+    return out
+
+
+def flip(img: torch.Tensor, sym: str) -> torch.Tensor:
+    """cv2.flip for symmetry.py's keys ('o' = copy)."""
+    return copy_window(img, None, SYM_FLIP[sym])
+
+
+# ---------------------------------------------------------------------------
+# Alpha bbox (Pillow getbbox alpha_only / cv2.findNonZero + boundingRect)
+# ---------------------------------------------------------------------------
+
+def alpha_bbox(imgs: Sequence[torch.Tensor]) -> List[Optional[Tuple[int, int, int, int]]]:
+    dev = imgs[0].device
+    n = len(imgs)
+    d = np.zeros(n, N.IMAGE_DESC)
+    flat = []
+    off = 0
+    for i, im in enumerate(imgs):
+        _require_cuda(im, "alpha_bbox")
+        h, w, cn = im.shape
+        d[i]["off"], d[i]["w"], d[i]["h"], d[i]["pitch"], d[i]["cn"] = off, w, h, w * cn, cn
+        flat.append(im.contiguous().reshape(-1))
+        off += h * w * cn
+    buf = torch.cat(flat) if n > 1 else flat[0]
+    bbox = torch.empty(4 * n, dtype=torch.int32, device=dev)
+    mw = max(int(im.shape[1]) for im in imgs)
+    mh = max(int(im.shape[0]) for im in imgs)
+    N.check(N.load().ipp_alpha_bbox(buf.data_ptr(), _to_dev(d, dev).data_ptr(), n, mw, mh, bbox.data_ptr(),
+                                    _stream(dev)), "ipp_alpha_bbox")
+    bb = bbox.cpu().numpy().reshape(n, 4)
+    return [None if r[0] < 0 else tuple(int(v) for v in r) for r in bb]
+
+
+# ---------------------------------------------------------------------------
+# HSV range mask (filtres_liste.py:84-134)
+# ---------------------------------------------------------------------------
+
+def hsv_mask(img: torch.Tensor, params: np.ndarray) -> torch.Tensor:
+    """img: (H, W, 3|4) in the channel order params['bgr'] names → (H, W, 4)."""
+    _require_cuda(img, "hsv_mask")
+    img = img.contiguous()
+    h, w, cn = img.shape
+    out = torch.empty((h, w, 4), dtype=torch.uint8, device=img.device)
+    sd = np.zeros(1, N.IMAGE_DESC)
+    sd[0]["w"], sd[0]["h"], sd[0]["pitch"], sd[0]["cn"] = w, h, w * cn, cn
+    dd = np.zeros(1, N.IMAGE_DESC)
+    dd[0]["w"], dd[0]["h"], dd[0]["pitch"], dd[0]["cn"] = w, h, 4 * w, 4
+    p = np.ascontiguousarray(params)
+    N.check(N.load().ipp_hsv_mask(img.data_ptr(), _to_dev(sd, img.device).data_ptr(), out.data_ptr(),
+                                  _to_dev(dd, img.device).data_ptr(), 1, w, h, N.np_ptr(p),
+                                  _stream(img.device)), "ipp_hsv_mask")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# LANCZOS resize of RGBA (overlays.py:129) and paste (overlays.py:138-139)
+# ---------------------------------------------------------------------------
+
+def resize_lanczos_rgba(img: torch.Tensor, out_w: int, out_h: int) -> torch.Tensor:
+    """Pillow ``Image.resize((out_w, out_h), LANCZOS)`` of an RGBA image."""
+    _require_cuda(img, "resize_lanczos_rgba")
+    img = img.contiguous()
+    in_h, in_w, cn = img.shape
+    if cn != 4:
+        raise ValueError("resize_lanczos_rgba expects RGBA")
+    if (in_w, in_h) == (out_w, out_h):
+        return img.clone()  # Image.py:2400: plain copy, no RGBa round trip
+    lib = N.load()
+    dev = img.device
+    need_h, need_v = out_w != in_w, out_h != in_h
+    kh, th = G.lanczos_taps(in_w, out_w)
+    kv, tv = G.lanczos_taps(in_h, out_h)
+    cur = img
+    if need_h:
+        y0 = int(tv[0])
+        y1 = int(tv[2 * out_h - 2] + tv[2 * out_h - 1])
+        tv = tv.copy()
+        tv[0:2 * out_h:2] -= y0
+        rows = y1 - y0
+        tmp = torch.empty((rows, out_w, 4), dtype=torch.uint8, device=dev)
+        d = np.zeros(1, N.RESAMPLE_DESC)
+        d[0]["src_pitch"], d[0]["dst_pitch"] = 4 * in_w, 4 * out_w
+        d[0]["in_len"], d[0]["out_len"], d[0]["lines"], d[0]["line0"], d[0]["ksize"] = in_w, out_w, rows, y0, kh
+        flags = N.IPP_RS_PREMULTIPLY | (0 if need_v else N.IPP_RS_UNPREMULTIPLY)
+        N.check(lib.ipp_lanczos_h(cur.data_ptr(), tmp.data_ptr(), _to_dev(th, dev).data_ptr(),
+                                  _to_dev(d, dev).data_ptr(), 1, out_w, rows, flags, _stream(dev)), "ipp_lanczos_h")
+        cur = tmp
+    if need_v:
+        out = torch.empty((out_h, out_w, 4), dtype=torch.uint8, device=dev)
+        d = np.zeros(1, N.RESAMPLE_DESC)
+        d[0]["src_pitch"], d[0]["dst_pitch"] = 4 * out_w, 4 * out_w
+        d[0]["in_len"], d[0]["out_len"], d[0]["lines"], d[0]["ksize"] = cur.shape[0], out_h, out_w, kv
+        flags = N.IPP_RS_UNPREMULTIPLY | (0 if need_h else N.IPP_RS_PREMULTIPLY)
+        N.check(lib.ipp_lanczos_v(cur.data_ptr(), out.data_ptr(), _to_dev(tv, dev).data_ptr(),
+                                  _to_dev(d, dev).data_ptr(), 1, out_h, out_w, flags, _stream(dev)), "ipp_lanczos_v")
+        cur = out
+    return cur
+
+
+def paste_blend(bg: torch.Tensor, ov: torch.Tensor, x: int, y: int) -> torch.Tensor:
+    """``bg.copy(); bg.paste(ov, (x, y), ov)`` for RGB bg and RGBA ov."""
+    _require_cuda(bg, "paste_blend")
+    _require_cuda(ov, "paste_blend")
+    bg = bg.contiguous()
+    ov = ov.contiguous()
+    bh, bw, _ = bg.shape
+    oh, ow, _ = ov.shape
+    if x < 0 or y < 0 or x + ow > bw or y + oh > bh:
+        raise ValueError("overlay must lie inside the background")
+    out = torch.empty_like(bg)
+    d = np.zeros(1, N.PASTE_DESC)
+    d[0]["bg_w"], d[0]["bg_h"], d[0]["bg_pitch"], d[0]["dst_pitch"] = bw, bh, 3 * bw, 3 * bw
+    d[0]["ov_w"], d[0]["ov_h"], d[0]["ov_pitch"], d[0]["x"], d[0]["y"] = ow, oh, 4 * ow, x, y
+    N.check(N.load().ipp_paste_blend(bg.data_ptr(), ov.data_ptr(), out.data_ptr(), _to_dev(d, bg.device).data_ptr(),
+                                     1, bw, bh, _stream(bg.device)), "ipp_paste_blend")
+    return out

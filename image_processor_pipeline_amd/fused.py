@@ -1,0 +1,234 @@
+"""Batched device mode of the 5-stage pipe (BASELINE configs 3 and 4).
+
+The reference runs five ``ProcessingStep``s chained through files
+(pipeline.py:526-541), each calling one transform per item:
+
+  1. recadrages.crop_from_border      (margin crop,          recadrages.py:13-61)
+  2. rotations.process_rotations      (RGBA, NEAREST rotate, bbox crop, rotations.py:6-133)
+  3. symmetry.generate_symmetries     (flip,                 symmetry.py:11-149)
+  4. filtres_liste.process_images_with_color_masks (HSV α,   filtres_liste.py:41-149)
+  5. overlays.paste_overlay_onto_background ('modulo' pairing with a cycled
+     background set, LANCZOS resize + alpha paste,           overlays.py:24-187)
+
+Here one host planning pass draws every random parameter in the reference's
+draw order (``draw_params``) and fills one ``ipp_pipe_desc`` per item; the
+device work is two launches for the whole batch (``ipp_pipe_hpass``,
+``ipp_pipe_vblend``).  Intermediate cut-outs never touch HBM.
+"""
+from __future__ import annotations
+
+import math
+import random
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import geometry as G
+from .device import SYM_FLIP, _stream, _to_dev
+
+ALL_SYMS = ("o", "h", "v", "hv")
+
+
+@dataclass
+class PipeConfig:
+    margins: Tuple[float, float, float, float] = (64, 64, 64, 64)   # crop_from_border crop_margins
+    angle_min: float = 1.0                                          # process_rotations defaults
+    angle_max: float = 359.0
+    sym_pool: Tuple[str, ...] = ALL_SYMS                             # generate_symmetries pool
+    hsv_ranges: list = field(default_factory=lambda: list(G.REFERENCE_HSV_RANGES))
+    zones: Optional[list] = None
+    use_gimp_scale: bool = False
+    scale_min: float = 0.15                                         # paste_overlay_onto_background
+    scale_max: float = 0.30
+
+
+@dataclass
+class ItemParams:
+    angle: float
+    sym: str
+    bg_index: int
+    ratio: float
+    x: int = 0
+    y: int = 0
+
+
+@dataclass
+class PipePlan:
+    descs: np.ndarray            # PIPE_DESC[n]
+    coefs: np.ndarray            # int32 taps for all items
+    hsv: np.ndarray              # HSV_PARAMS
+    params: List[ItemParams]
+    cut_dims: List[Tuple[int, int]]       # (h, w) of the cut-out M
+    ov_dims: List[Tuple[int, int]]        # (h, w) of the resized overlay
+    tmp_bytes: int
+    max_out_w: int
+    max_rows: int
+    bg_w: int
+    bg_h: int
+    algo_bytes_hpass: int = 0
+    algo_bytes_vblend: int = 0
+
+
+def draw_params(n: int, src_hw: Tuple[int, int], bg_hw: Tuple[int, int], n_bg: int, cfg: PipeConfig,
+                seed: int) -> Tuple[List[ItemParams], List[Tuple]]:
+    """Per-item random parameters in the reference's draw order.
+
+    pipeline.py:202 shuffles the background list once ('modulo' pairing);
+    per item: rotations.py:89 uniform, symmetry.py:122 sample(pool, 1),
+    overlays.py:108 uniform, :133-134 randint × 2.  The draws that depend on
+    geometry (positions) are resolved during planning (see plan_pipe)."""
+    rng = random.Random(seed)
+    order = list(range(n_bg))
+    rng.shuffle(order)
+    return rng, order
+
+
+def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int, cfg: PipeConfig,
+              seed: int = 0, src_pitch: Optional[int] = None) -> PipePlan:
+    H, W = src_hw
+    bh, bw = bg_hw
+    rng, order = draw_params(n, src_hw, bg_hw, n_bg, cfg, seed)
+    t, b, l, r = G.crop_margins(H, W, cfg.margins)
+    wc, hc = W - l - r, H - t - b
+    d = np.zeros(n, N.PIPE_DESC)
+    params: List[ItemParams] = []
+    cut_dims, ov_dims = [], []
+    # axis list for the batch tap planner: (in, out) pairs, H then V per item
+    axes_in, axes_out, identity = [], [], []
+    rot_cache = {}
+    for i in range(n):
+        angle = rng.uniform(cfg.angle_min, cfg.angle_max)
+        sym = rng.sample(list(cfg.sym_pool), 1)[0]
+        key = angle
+        plan = G.rotation_plan(wc, hc, angle)
+        bb = G.rotated_bbox(wc, hc, plan)
+        if bb is not None and bb[2] > bb[0] and bb[3] > bb[1]:
+            ox, oy, rw, rh = bb[0], bb[1], bb[2] - bb[0], bb[3] - bb[1]
+        else:
+            ox, oy, rw, rh = 0, 0, plan.nw, plan.nh
+        ratio = rng.uniform(cfg.scale_min, cfg.scale_max)
+        nw_, nh_ = G.overlay_size(rw, rh, bw, bh, ratio)
+        if nw_ <= 0 or nh_ <= 0:
+            raise ValueError(f"item {i}: degenerate overlay size {nw_}x{nh_}")
+        x = rng.randint(0, bw - nw_)
+        y = rng.randint(0, bh - nh_)
+        params.append(ItemParams(angle, sym, order[i % n_bg], ratio, x, y))
+        cut_dims.append((rh, rw))
+        ov_dims.append((nh_, nw_))
+        g = d[i]["g"]
+        g["src_off"] = i * H * (src_pitch or 3 * W)
+        g["src_pitch"] = src_pitch or 3 * W
+        g["src_cn"] = 3
+        g["src_w"], g["src_h"] = W, H
+        g["in_x0"], g["in_y0"], g["in_w"], g["in_h"] = l, t, wc, hc
+        for k in range(6):
+            g[f"a{k}"] = plan.A[k]
+        g["out_w"], g["out_h"] = rw, rh
+        g["off_x"], g["off_y"] = ox, oy
+        g["flip"] = SYM_FLIP[sym]
+        same = (nw_, nh_) == (rw, rh)
+        identity.append((same or nw_ == rw, same or nh_ == rh))
+        axes_in += [rw, rh]
+        axes_out += [nw_, nh_]
+
+    # ---- taps (C planner, threaded) -------------------------------------
+    lib = N.load()
+    sizes = np.zeros(2 * n, np.int64)
+    ks = np.zeros(2 * n, np.int64)
+    for j in range(2 * n):
+        idn = identity[j // 2][j % 2]
+        k = 1 if idn else lib.ipp_plan_lanczos_ksize(0.0, float(axes_in[j]), axes_out[j])
+        ks[j] = k
+        sizes[j] = 2 * axes_out[j] + axes_out[j] * k
+    offs = np.zeros(2 * n, np.int64)
+    offs[1:] = np.cumsum(sizes)[:-1]
+    coefs = np.zeros(int(sizes.sum()), np.int32)
+    sel = np.array([not identity[j // 2][j % 2] for j in range(2 * n)])
+    idx = np.flatnonzero(sel)
+    if idx.size:
+        ins = np.array([axes_in[j] for j in idx], np.int32)
+        outs = np.array([axes_out[j] for j in idx], np.int32)
+        o = offs[idx].astype(np.int64)
+        N.check(lib.ipp_plan_lanczos_batch(len(idx), N.np_ptr(ins), N.np_ptr(outs), N.np_ptr(o), N.np_ptr(coefs),
+                                           coefs.size, 0), "ipp_plan_lanczos_batch")
+    for j in np.flatnonzero(~sel):
+        _, buf = G.identity_taps(axes_out[j])
+        coefs[offs[j]:offs[j] + buf.size] = buf
+
+    # ---- descriptors ----------------------------------------------------
+    tmp_off = 0
+    max_out_w = max_rows = 1
+    algo_h = algo_v = 0
+    for i in range(n):
+        rh, rw = cut_dims[i]
+        nh_, nw_ = ov_dims[i]
+        jh, jv = 2 * i, 2 * i + 1
+        vb = coefs[offs[jv]:offs[jv] + 2 * nh_]
+        need_h = not identity[i][0]
+        if need_h:
+            y0 = int(vb[0])
+            y1 = int(vb[2 * nh_ - 2] + vb[2 * nh_ - 1])
+            vb[0::2] -= y0
+        else:
+            y0, y1 = 0, rh
+        rows = y1 - y0
+        h = d[i]["h"]
+        h["dst_off"] = tmp_off
+        h["dst_pitch"] = 4 * nw_
+        h["in_len"], h["out_len"], h["lines"], h["line0"], h["ksize"] = rw, nw_, rows, y0, ks[jh]
+        h["coef_off"] = offs[jh]
+        v = d[i]["v"]
+        v["src_off"] = tmp_off
+        v["src_pitch"] = 4 * nw_
+        v["in_len"], v["out_len"], v["lines"], v["ksize"] = rows, nh_, nw_, ks[jv]
+        v["coef_off"] = offs[jv]
+        p = d[i]["p"]
+        it = params[i]
+        p["bg_off"] = it.bg_index * bh * bw * 3
+        p["dst_off"] = i * bh * bw * 3
+        p["bg_w"], p["bg_h"], p["bg_pitch"], p["dst_pitch"] = bw, bh, 3 * bw, 3 * bw
+        p["ov_w"], p["ov_h"], p["ov_pitch"], p["x"], p["y"] = nw_, nh_, 4 * nw_, it.x, it.y
+        tmp_off += 4 * nw_ * rows
+        tmp_off = (tmp_off + 255) // 256 * 256
+        max_out_w = max(max_out_w, nw_)
+        max_rows = max(max_rows, rows)
+        algo_h += 3 * hc * wc + 4 * nw_ * rows
+        algo_v += 4 * nw_ * rows + 3 * bh * bw + 3 * bh * bw
+    hsv = G.hsv_params(cfg.hsv_ranges, cfg.zones, cfg.use_gimp_scale, bgr=False)
+    return PipePlan(d, coefs, hsv, params, cut_dims, ov_dims, max(tmp_off, 256), max_out_w, max_rows, bw, bh,
+                    algo_h, algo_v)
+
+
+class PipeRunner:
+    """Device-resident plan + scratch for repeated runs of one batch."""
+
+    def __init__(self, plan: PipePlan, device):
+        self.plan = plan
+        self.device = torch.device(device)
+        self.descs = _to_dev(plan.descs, self.device)
+        self.coefs = torch.from_numpy(plan.coefs).to(self.device)
+        self.tmp = torch.empty(plan.tmp_bytes, dtype=torch.uint8, device=self.device)
+        self.lib = N.load()
+
+    def hpass(self, src: torch.Tensor) -> None:
+        p = self.plan
+        N.check(self.lib.ipp_pipe_hpass(src.data_ptr(), self.tmp.data_ptr(), self.coefs.data_ptr(),
+                                        self.descs.data_ptr(), len(p.descs), p.max_out_w, p.max_rows,
+                                        N.np_ptr(p.hsv), _stream(self.device)), "ipp_pipe_hpass")
+
+    def vblend(self, bgs: torch.Tensor, out: torch.Tensor) -> None:
+        p = self.plan
+        N.check(self.lib.ipp_pipe_vblend(self.tmp.data_ptr(), bgs.data_ptr(), out.data_ptr(), self.coefs.data_ptr(),
+                                         self.descs.data_ptr(), len(p.descs), p.bg_w, p.bg_h,
+                                         _stream(self.device)), "ipp_pipe_vblend")
+
+    def run(self, src: torch.Tensor, bgs: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        for t, name in ((src, "src"), (bgs, "bgs"), (out, "out")):
+            if not (t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous()):
+                raise N.NativeUnavailable(f"PipeRunner.run: {name} must be a contiguous uint8 ROCm tensor")
+        self.hpass(src)
+        self.vblend(bgs, out)
+        return out

@@ -1,0 +1,234 @@
+/*
+ * ipp.h — C ABI of the MI355X-native image_processor_pipeline hot path.
+ *
+ * The reference (Tezahc/image_processor_pipeline) is pure Python: its pixel
+ * arithmetic lives in Pillow's and OpenCV's C routines, called from the
+ * transforms plugins.  Each entry point below replaces one of those library
+ * calls (or a fused chain of them); the reference call site it stands in for
+ * is cited on each declaration.  The Python host layer
+ * (image_processor_pipeline_amd/) keeps the reference's plugin signatures and
+ * binds these symbols with ctypes.
+ *
+ * Conventions
+ *   - Images are HWC uint8 in caller-owned DEVICE memory; every pointer is a
+ *     device pointer, every size is in bytes/pixels as named.
+ *   - Batched calls take a DEVICE array of per-image descriptors, so one launch
+ *     covers a ragged batch.  Nothing here allocates persistent memory: scratch
+ *     is caller-provided.  All calls are asynchronous and stream-ordered on the
+ *     given hipStream_t (passed as void*), reentrant, and graph-capturable.
+ *   - Return value: 0 on success, a negative IPP_E* code otherwise (the Python
+ *     wrappers map codes to the exceptions the reference raises).
+ *   - Host-side planning helpers (ipp_plan_*) run on the CPU and fill
+ *     descriptors / tap tables; they reproduce the library's host arithmetic
+ *     bit-for-bit (double precision, same libm).
+ */
+#ifndef IPP_H
+#define IPP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IPP_OK 0
+#define IPP_E_ARG (-1)      /* invalid argument (null pointer, bad size)      */
+#define IPP_E_LAUNCH (-2)   /* HIP launch / runtime error                     */
+#define IPP_E_RANGE (-3)    /* geometry outside the supported fixed-point range */
+
+#define IPP_MAX_HSV_RANGES 16
+
+/* ------------------------------------------------------------------------ */
+/* K1+K2+K3+K4+K5: crop → RGBA → NEAREST rotate (expand) → bbox crop → flip  */
+/* ------------------------------------------------------------------------ */
+/* One image of the ragged batch.  The rotated canvas pixel (X, Y) reads
+ *   xin = (a2 + Y*a1 + X*a0) >> 16,  yin = (a5 + Y*a4 + X*a3) >> 16
+ * (int32 arithmetic, exactly Pillow Geometry.c affine_fixed) from the crop
+ * window [in_x0, in_x0+in_w) × [in_y0, in_y0+in_h) of the source, or writes
+ * (0,0,0,0) when (xin, yin) falls outside it.  Output pixel (x, y) is canvas
+ * pixel (off_x + fx, off_y + fy) with fx = flip&1 ? out_w-1-x : x and
+ * fy = flip&2 ? out_h-1-y : y.  Pillow's 0/90/180/270 fast paths are encoded
+ * with exact integer coefficients by ipp_plan_rotate.                        */
+typedef struct ipp_gather_desc {
+    int64_t src_off;   /* byte offset of this image's source in src         */
+    int64_t dst_off;   /* byte offset of this image's output in dst         */
+    int32_t src_pitch; /* bytes per source row                              */
+    int32_t src_cn;    /* source channels: 3 (RGB) or 4 (RGBA)              */
+    int32_t src_w, src_h; /* full source dims (bounds the wide loads)       */
+    int32_t in_x0, in_y0, in_w, in_h; /* crop window = image seen by rotate */
+    int32_t a0, a1, a2, a3, a4, a5;   /* 16.16 inverse affine               */
+    int32_t out_w, out_h;             /* output dims (after the bbox crop)  */
+    int32_t off_x, off_y;             /* bbox origin inside the canvas      */
+    int32_t flip;                     /* bit0: mirror x ('h'), bit1: mirror y ('v') */
+    int32_t dst_pitch;                /* bytes per output row (≥ 4*out_w)   */
+} ipp_gather_desc;
+
+/* rotations.py:55 convert('RGBA') + :96 rotate(angle, expand=True) + :99-101
+ * getbbox()/crop(), recadrages.py:46 margin crop, symmetry.py:114-119 flip —
+ * fused gather.  Writes RGBA. */
+int ipp_rotate_flip_nearest(const uint8_t* src, uint8_t* dst,
+                            const ipp_gather_desc* descs, int32_t n_images,
+                            int32_t max_out_w, int32_t max_out_h, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Plain 2-D window copy / flip (recadrages.py:46 slice, crop_square.py:196  */
+/* slice, symmetry.py:114-119 cv2.flip codes 1/0/-1, pixels_isolés.py:81).   */
+/* ------------------------------------------------------------------------ */
+typedef struct ipp_copy_desc {
+    int64_t src_off, dst_off;
+    int32_t src_pitch, dst_pitch;
+    int32_t x0, y0, w, h;   /* window in the source (pixels)               */
+    int32_t cn;             /* bytes per pixel (1..4)                       */
+    int32_t flip;           /* bit0 mirror x, bit1 mirror y                 */
+} ipp_copy_desc;
+
+int ipp_copy_window(const uint8_t* src, uint8_t* dst, const ipp_copy_desc* descs,
+                    int32_t n_images, int32_t max_w, int32_t max_h, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* K6+K7: OpenCV BGR2HSV (8-bit) + inRange × R + zone AND + OR + NOT → alpha */
+/* filtres_liste.py:84 imread(BGR) :90 cvtColor :97-123 inRange/zone/OR/NOT  */
+/* :132-134 merge(b, g, r, alpha).                                           */
+/* ------------------------------------------------------------------------ */
+typedef struct ipp_hsv_range {
+    int32_t lo[3], hi[3];   /* inRange bounds already prepared like cv::inRange
+                               (cvRound'ed, saturated; empty → lo=1, hi=0)   */
+    int32_t zone[4];        /* (top, bottom, left, right) margins; NumPy slice
+                               semantics rows[top:H-bottom], cols[left:W-right] */
+} ipp_hsv_range;
+
+typedef struct ipp_hsv_params {
+    int32_t n_ranges;
+    int32_t bgr;            /* 1: input channel order is B,G,R (cv2); 0: R,G,B */
+    ipp_hsv_range r[IPP_MAX_HSV_RANGES];
+} ipp_hsv_params;
+
+typedef struct ipp_image_desc {
+    int64_t off;            /* byte offset in the buffer                    */
+    int32_t w, h, pitch;    /* dims, bytes per row                          */
+    int32_t cn;             /* channels                                     */
+} ipp_image_desc;
+
+/* src: 3- or 4-channel images (an input alpha is dropped, as cv2.imread
+ * IMREAD_COLOR does); dst: 4-channel (same channel order + new alpha). */
+int ipp_hsv_mask(const uint8_t* src, const ipp_image_desc* src_descs,
+                 uint8_t* dst, const ipp_image_desc* dst_descs, int32_t n_images,
+                 int32_t max_w, int32_t max_h, const ipp_hsv_params* params, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* K8: Pillow resize(LANCZOS) of RGBA — separable 8bpc passes                */
+/* overlays.py:129 (PIL Image.resize → RGBa convert → ImagingResample H,V →  */
+/* RGBA convert).  Taps are int32 (22-bit fixed point) from ipp_plan_lanczos. */
+/* ------------------------------------------------------------------------ */
+typedef struct ipp_resample_desc {
+    int64_t src_off, dst_off;
+    int32_t src_pitch, dst_pitch;
+    int32_t in_len;         /* H pass: input width;  V pass: input height     */
+    int32_t out_len;        /* H pass: output width; V pass: output height    */
+    int32_t lines;          /* H pass: rows processed; V pass: columns        */
+    int32_t line0;          /* H pass: first source row (ybox_first)          */
+    int32_t ksize;          /* taps per output sample                         */
+    int32_t pad_;
+    int64_t coef_off;       /* int32 index of this image's bounds in coefs:
+                               bounds[2*out_len] (xmin, count) then
+                               taps[out_len*ksize]                            */
+} ipp_resample_desc;
+
+/* flags */
+#define IPP_RS_PREMULTIPLY 1   /* apply rgbA2rgba on the input (H pass)      */
+#define IPP_RS_UNPREMULTIPLY 2 /* apply rgba2rgbA on the output (V pass)     */
+
+int ipp_lanczos_h(const uint8_t* src, uint8_t* dst, const int32_t* coefs,
+                  const ipp_resample_desc* descs, int32_t n_images,
+                  int32_t max_out, int32_t max_lines, int32_t flags, void* stream);
+int ipp_lanczos_v(const uint8_t* src, uint8_t* dst, const int32_t* coefs,
+                  const ipp_resample_desc* descs, int32_t n_images,
+                  int32_t max_out, int32_t max_lines, int32_t flags, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* K9: background.copy() + paste(ov, (x, y), ov) onto RGB                     */
+/* overlays.py:138-139 (Paste.c paste_mask_RGBA, BLEND = DIV255).             */
+/* ------------------------------------------------------------------------ */
+typedef struct ipp_paste_desc {
+    int64_t bg_off, ov_off, dst_off;
+    int32_t bg_w, bg_h, bg_pitch, dst_pitch;
+    int32_t ov_w, ov_h, ov_pitch;
+    int32_t x, y;           /* paste position (must fit inside the bg)        */
+    int32_t pad_;
+} ipp_paste_desc;
+
+int ipp_paste_blend(const uint8_t* bg, const uint8_t* ov, uint8_t* dst,
+                    const ipp_paste_desc* descs, int32_t n_images,
+                    int32_t bg_w, int32_t bg_h, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Fused 5-stage pipe (configs 3/4): crop → rotate → flip → HSV mask →        */
+/* LANCZOS H pass, all computed on the fly from the source (the RGBA cut-out  */
+/* is never materialised); then LANCZOS V pass → unpremultiply → paste onto   */
+/* the background, fused with the background copy.                           */
+/* ------------------------------------------------------------------------ */
+typedef struct ipp_pipe_desc {
+    ipp_gather_desc g;      /* stage 1-3 (dst fields unused)                  */
+    ipp_resample_desc h;    /* H pass: src = the virtual cut-out, dst = tmp   */
+    ipp_resample_desc v;    /* V pass: src = tmp                              */
+    ipp_paste_desc p;       /* paste: ov = V-pass result (never stored)        */
+} ipp_pipe_desc;
+
+int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
+                   const ipp_pipe_desc* descs, int32_t n_images,
+                   int32_t max_out_w, int32_t max_rows,
+                   const ipp_hsv_params* hsv, void* stream);
+int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
+                    const int32_t* coefs, const ipp_pipe_desc* descs, int32_t n_images,
+                    int32_t bg_w, int32_t bg_h, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* K10-K13: pixels_isolés.keep_largest_component                             */
+/* :32 threshold(α,1,255) :35 connectedComponentsWithStats(8) :38-55 keep    */
+/* largest :74-81 crop-fit (findNonZero + boundingRect).                     */
+/* ------------------------------------------------------------------------ */
+/* labels: int32 scratch, w*h per image (caller-provided, at image_desc.off/cn
+ * scaled: label index base = lab_off[i]).  stats: int64 scratch of
+ * 8 words per image (best key, bbox).  Output: α outside the largest
+ * component zeroed IN PLACE in img; bbox[i] = (x0, y0, x1, y1) of α≠0 or
+ * (-1,-1,-1,-1) when the image has no α≠0 pixel. */
+int ipp_ccl_keep_largest(uint8_t* img, const ipp_image_desc* descs, int32_t n_images,
+                         int32_t max_w, int32_t max_h, int32_t* labels,
+                         const int64_t* lab_off, uint32_t* area, int64_t* stats,
+                         int32_t* bbox, void* stream);
+
+/* Alpha bbox (Pillow getbbox alpha_only / cv2.findNonZero+boundingRect) of
+ * 4-channel images: bbox[i] = (x0, y0, x1, y1) or (-1,-1,-1,-1). */
+int ipp_alpha_bbox(const uint8_t* img, const ipp_image_desc* descs, int32_t n_images,
+                   int32_t max_w, int32_t max_h, int32_t* bbox, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Host-side planning (CPU).                                                 */
+/* ------------------------------------------------------------------------ */
+/* Pillow Resample.c precompute_coeffs + normalize_coeffs_8bpc for LANCZOS
+ * (support 3): writes bounds[2*out_size] (xmin, count) followed by
+ * taps[out_size*ksize] into `out` (int32); returns ksize, or the required
+ * int32 count when out == NULL (as -count), or IPP_E_ARG. */
+int64_t ipp_plan_lanczos(int32_t in_size, double in0, double in1, int32_t out_size,
+                         int32_t* out, int64_t out_capacity);
+/* Batch form: n axes (in_sizes[i] → out_sizes[i], box = full axis), each
+ * written at int32 offset offsets[i] of `out`; n_threads ≤ 0 = all cores. */
+int ipp_plan_lanczos_batch(int32_t n, const int32_t* in_sizes, const int32_t* out_sizes,
+                           const int64_t* offsets, int32_t* out, int64_t out_capacity,
+                           int32_t n_threads);
+/* ksize for (in_size, out_size) without computing taps. */
+int32_t ipp_plan_lanczos_ksize(double in0, double in1, int32_t out_size);
+
+/* Alpha bbox of the rotated canvas of a fully opaque in_w×in_h image under
+ * the 16.16 affine (a0..a5) on an nw×nh canvas, computed analytically per
+ * row with exact integer arithmetic.  bbox = (x0, y0, x1, y1) or all -1. */
+int ipp_plan_opaque_bbox(int32_t in_w, int32_t in_h, const int32_t a[6],
+                         int32_t nw, int32_t nh, int32_t bbox[4]);
+
+/* Library version / build info string. */
+const char* ipp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IPP_H */

@@ -1,0 +1,72 @@
+"""Pin the CPU oracle against golden vectors from Pillow 12.2.0 and the
+reference's own rotations.py / overlays.py (tools/make_goldens.py)."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import ops
+from tests.conftest import unpack
+
+
+def test_rotate_canvas_and_bbox_match_pillow(golden):
+    g = golden("rotate_pillow.npz")
+    srcs = unpack(g["src_flat"], g["src_shapes"])
+    outs = unpack(g["out_flat"], g["out_shapes"])
+    assert len(outs) == len(g["angles"]) > 100
+    for out, si, a, bb in zip(outs, g["src_index"], g["angles"], g["bboxes"]):
+        src = ops.to_rgba(srcs[si])
+        got = ops.rotate_expand_nearest(src, float(a))
+        assert got.shape == out.shape, (si, a)
+        assert np.array_equal(got, out), (si, a)
+        gbb = ops.getbbox_alpha(got)
+        assert (gbb if gbb is not None else (-1, -1, -1, -1)) == tuple(bb)
+
+
+def test_process_rotations_reference_outputs(golden):
+    g = golden("rotations_ref.npz")
+    outs = unpack(g["out_flat"], g["out_shapes"])
+    names = list(g["names"])
+    src = ops.to_rgba(g["src"])
+    # r000 = original (rotations.py:77-85), then one file per angle draw (:88-119)
+    assert names[0].endswith("_r000.png") and np.array_equal(outs[0], src)
+    random.seed(int(g["seed"]))
+    for i, out in enumerate(outs[1:], start=1):
+        a = random.uniform(1.0, 359.0)
+        assert a == g["angles"][i - 1]
+        assert names[i].endswith(f"_r{i:03d}.png")
+        assert np.array_equal(ops.rotate_and_crop(src, a), out)
+
+
+def test_lanczos_resize_matches_pillow(golden):
+    g = golden("resize_pillow.npz")
+    srcs = unpack(g["src_flat"], g["src_shapes"])
+    outs = unpack(g["out_flat"], g["out_shapes"])
+    for s, o, (ow, oh) in zip(srcs, outs, g["sizes"]):
+        got = ops.resize_lanczos_rgba(s, int(ow), int(oh))
+        assert np.array_equal(got, o), (s.shape, ow, oh)
+
+
+def test_paste_matches_pillow(golden):
+    g = golden("paste_pillow.npz")
+    for (x, y), out in zip(g["pos"], g["outs"]):
+        got = ops.paste_rgba_onto_rgb(g["bg"], g["ov"], int(x), int(y))
+        assert np.array_equal(got, out[..., :3])
+
+
+def test_overlay_reference_composite_and_label(golden):
+    g = golden("overlays_ref.npz")
+    ovs = unpack(g["ov_flat"], g["ov_shapes"])
+    bgs = unpack(g["bg_flat"], g["bg_shapes"])
+    comps = unpack(g["comp_flat"], g["comp_shapes"])
+    for ov, bg, comp, label, seed in zip(ovs, bgs, comps, g["labels"], g["seeds"]):
+        random.seed(int(seed))
+        ratio = random.uniform(0.15, 0.30)
+        bh, bw = bg.shape[:2]
+        nw, nh = ops.overlay_geometry(ov.shape[1], ov.shape[0], bw, bh, ratio)
+        x = random.randint(0, bw - nw)
+        y = random.randint(0, bh - nh)
+        rs = ops.resize_lanczos_rgba(ov, nw, nh)
+        got = ops.paste_rgba_onto_rgb(bg, rs, x, y)
+        assert np.array_equal(got, comp)
+        assert ops.yolo_label(0, x, y, nw, nh, bw, bh) == str(label)
