@@ -27,6 +27,14 @@ def _to_dev(a: np.ndarray, device) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(device)
 
 
+def _keep(*tensors: torch.Tensor) -> None:
+    """Tie small device buffers (descriptors, taps) to the current stream so
+    the caching allocator cannot hand their memory to a later H2D copy before
+    the kernels that read them have run."""
+    for t in tensors:
+        t.record_stream(torch.cuda.current_stream(t.device))
+
+
 def _require_cuda(t: torch.Tensor, name: str) -> None:
     if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.uint8):
         raise N.NativeUnavailable(f"{name}: expected a uint8 tensor on a ROCm device (no CPU fallback)")
@@ -156,6 +164,7 @@ def copy_window(img: torch.Tensor, window: Optional[Tuple[int, int, int, int]] =
     dd = _to_dev(d, img.device)
     N.check(N.load().ipp_copy_window(img.data_ptr(), out.data_ptr(), dd.data_ptr(), 1, ww, wh,
                                      _stream(img.device)), "ipp_copy_window")
+    _keep(dd)
     return out
 
 
@@ -184,7 +193,8 @@ def alpha_bbox(imgs: Sequence[torch.Tensor]) -> List[Optional[Tuple[int, int, in
     bbox = torch.empty(4 * n, dtype=torch.int32, device=dev)
     mw = max(int(im.shape[1]) for im in imgs)
     mh = max(int(im.shape[0]) for im in imgs)
-    N.check(N.load().ipp_alpha_bbox(buf.data_ptr(), _to_dev(d, dev).data_ptr(), n, mw, mh, bbox.data_ptr(),
+    dd = _to_dev(d, dev)
+    N.check(N.load().ipp_alpha_bbox(buf.data_ptr(), dd.data_ptr(), n, mw, mh, bbox.data_ptr(),
                                     _stream(dev)), "ipp_alpha_bbox")
     bb = bbox.cpu().numpy().reshape(n, 4)
     return [None if r[0] < 0 else tuple(int(v) for v in r) for r in bb]
@@ -205,9 +215,10 @@ def hsv_mask(img: torch.Tensor, params: np.ndarray) -> torch.Tensor:
     dd = np.zeros(1, N.IMAGE_DESC)
     dd[0]["w"], dd[0]["h"], dd[0]["pitch"], dd[0]["cn"] = w, h, 4 * w, 4
     p = np.ascontiguousarray(params)
-    N.check(N.load().ipp_hsv_mask(img.data_ptr(), _to_dev(sd, img.device).data_ptr(), out.data_ptr(),
-                                  _to_dev(dd, img.device).data_ptr(), 1, w, h, N.np_ptr(p),
-                                  _stream(img.device)), "ipp_hsv_mask")
+    sdd, ddd = _to_dev(sd, img.device), _to_dev(dd, img.device)
+    N.check(N.load().ipp_hsv_mask(img.data_ptr(), sdd.data_ptr(), out.data_ptr(), ddd.data_ptr(), 1, w, h,
+                                  N.np_ptr(p), _stream(img.device)), "ipp_hsv_mask")
+    _keep(sdd, ddd)
     return out
 
 
@@ -241,8 +252,10 @@ def resize_lanczos_rgba(img: torch.Tensor, out_w: int, out_h: int) -> torch.Tens
         d[0]["src_pitch"], d[0]["dst_pitch"] = 4 * in_w, 4 * out_w
         d[0]["in_len"], d[0]["out_len"], d[0]["lines"], d[0]["line0"], d[0]["ksize"] = in_w, out_w, rows, y0, kh
         flags = N.IPP_RS_PREMULTIPLY | (0 if need_v else N.IPP_RS_UNPREMULTIPLY)
-        N.check(lib.ipp_lanczos_h(cur.data_ptr(), tmp.data_ptr(), _to_dev(th, dev).data_ptr(),
-                                  _to_dev(d, dev).data_ptr(), 1, out_w, rows, flags, _stream(dev)), "ipp_lanczos_h")
+        thd, dd = _to_dev(th, dev), _to_dev(d, dev)
+        N.check(lib.ipp_lanczos_h(cur.data_ptr(), tmp.data_ptr(), thd.data_ptr(), dd.data_ptr(), 1, out_w, rows,
+                                  flags, _stream(dev)), "ipp_lanczos_h")
+        _keep(thd, dd)
         cur = tmp
     if need_v:
         out = torch.empty((out_h, out_w, 4), dtype=torch.uint8, device=dev)
@@ -250,8 +263,10 @@ def resize_lanczos_rgba(img: torch.Tensor, out_w: int, out_h: int) -> torch.Tens
         d[0]["src_pitch"], d[0]["dst_pitch"] = 4 * out_w, 4 * out_w
         d[0]["in_len"], d[0]["out_len"], d[0]["lines"], d[0]["ksize"] = cur.shape[0], out_h, out_w, kv
         flags = N.IPP_RS_UNPREMULTIPLY | (0 if need_h else N.IPP_RS_PREMULTIPLY)
-        N.check(lib.ipp_lanczos_v(cur.data_ptr(), out.data_ptr(), _to_dev(tv, dev).data_ptr(),
-                                  _to_dev(d, dev).data_ptr(), 1, out_h, out_w, flags, _stream(dev)), "ipp_lanczos_v")
+        tvd, dd = _to_dev(tv, dev), _to_dev(d, dev)
+        N.check(lib.ipp_lanczos_v(cur.data_ptr(), out.data_ptr(), tvd.data_ptr(), dd.data_ptr(), 1, out_h, out_w,
+                                  flags, _stream(dev)), "ipp_lanczos_v")
+        _keep(tvd, dd)
         cur = out
     return cur
 
@@ -270,6 +285,8 @@ def paste_blend(bg: torch.Tensor, ov: torch.Tensor, x: int, y: int) -> torch.Ten
     d = np.zeros(1, N.PASTE_DESC)
     d[0]["bg_w"], d[0]["bg_h"], d[0]["bg_pitch"], d[0]["dst_pitch"] = bw, bh, 3 * bw, 3 * bw
     d[0]["ov_w"], d[0]["ov_h"], d[0]["ov_pitch"], d[0]["x"], d[0]["y"] = ow, oh, 4 * ow, x, y
-    N.check(N.load().ipp_paste_blend(bg.data_ptr(), ov.data_ptr(), out.data_ptr(), _to_dev(d, bg.device).data_ptr(),
-                                     1, bw, bh, _stream(bg.device)), "ipp_paste_blend")
+    dd = _to_dev(d, bg.device)
+    N.check(N.load().ipp_paste_blend(bg.data_ptr(), ov.data_ptr(), out.data_ptr(), dd.data_ptr(), 1, bw, bh,
+                                     _stream(bg.device)), "ipp_paste_blend")
+    _keep(dd)
     return out

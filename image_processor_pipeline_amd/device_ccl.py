@@ -50,10 +50,10 @@ def keep_largest_masks(imgs: Sequence[torch.Tensor]) -> List[Optional[Tuple[int,
     bbox = torch.empty(4 * n, dtype=torch.int32, device=dev)
     mw = max(int(im.shape[1]) for im in imgs)
     mh = max(int(im.shape[0]) for im in imgs)
-    N.check(N.load().ipp_ccl_keep_largest(buf.data_ptr(), _to_dev(d, dev).data_ptr(), n, mw, mh,
-                                          labels.data_ptr(), _to_dev(lab_off, dev).data_ptr(), area.data_ptr(),
-                                          stats.data_ptr(), bbox.data_ptr(), _stream(dev)),
-            "ipp_ccl_keep_largest")
+    dd, lo = _to_dev(d, dev), _to_dev(lab_off, dev)
+    N.check(N.load().ipp_ccl_keep_largest(buf.data_ptr(), dd.data_ptr(), n, mw, mh, labels.data_ptr(),
+                                          lo.data_ptr(), area.data_ptr(), stats.data_ptr(), bbox.data_ptr(),
+                                          _stream(dev)), "ipp_ccl_keep_largest")
     off = 0
     for im in imgs:  # write back when the inputs were not contiguous views of buf
         sz = im.numel()
