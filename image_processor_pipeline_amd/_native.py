@@ -15,7 +15,7 @@ from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).resolve().parent / "libipp.so"
+LIB_PATH = Path(os.environ.get("IPP_LIB_PATH", str(Path(__file__).resolve().parent / "libipp.so")))
 
 IPP_OK = 0
 IPP_E_ARG = -1
@@ -89,6 +89,10 @@ SIGNATURES = {
     "ipp_plan_lanczos_ksize": (_I, [_D, _D, _I]),
     "ipp_plan_lanczos_batch": (_I, [_I, _P, _P, _P, _P, _L, _I]),
     "ipp_plan_opaque_bbox": (_I, [_I, _I, _P, _I, _I, _P]),
+    "ipp_plan_dot4_stride": (_I, [_I]),
+    "ipp_plan_dot4_size": (_L, [_I, _I]),
+    "ipp_plan_dot4_from_taps": (_I, [_I, _I, _P, _I, _P]),
+    "ipp_plan_pipe_axes": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _I]),
     "ipp_version": (ctypes.c_char_p, []),
 }
 

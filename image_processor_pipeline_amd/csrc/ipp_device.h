@@ -69,8 +69,16 @@ __device__ __forceinline__ uint32_t unpremultiply(uint32_t px) {
 }
 
 // Resample.c clip8: clamp(ss >> 22, 0, 255) with an arithmetic shift.
+//
+// The empty asm is an optimisation barrier: ROCm 7.2's gfx950 backend fuses
+// "clamp(a >> 22) | clamp(b >> 22) << 8" into v_ashr_pk_u8_i32 and then ORs
+// further bytes into bits 16-31 of that register as if the instruction had
+// zeroed them; on MI355X the upper half keeps its previous contents, which
+// corrupted bytes 2/3 of packed results (found by tests/test_gpu_parity.py,
+// diagnosed in DESIGN.md §Toolchain notes).
 __device__ __forceinline__ uint32_t clip8(int32_t ss) {
     int32_t v = ss >> 22;
+    asm volatile("" : "+v"(v));
     return (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 

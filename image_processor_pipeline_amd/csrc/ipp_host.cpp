@@ -173,3 +173,123 @@ extern "C" int ipp_plan_opaque_bbox(int32_t in_w, int32_t in_h, const int32_t a[
 }
 
 extern "C" const char* ipp_version(void) { return "ipp 0.1.0 (gfx950)"; }
+
+// ---------------------------------------------------------------------------
+// dot4 tap format (fused pipe kernels).  For output o with Pillow taps
+// k[0..cnt) starting at input index xmin (optionally shifted by `shift`):
+//   hdr[o]    = (g0, ng, bias, 0)   g0 = (xmin-shift) & ~3 (4-aligned start),
+//                                   ng = ceil(((xmin-shift)&3) + cnt) / 4),
+//                                   bias = 2^21 + 128 * Σk
+//   planes[o][j] = (P0, P1, P2, 0)  byte b of Pp = balanced signed byte p of
+//                                   tap (4j + b - ((xmin-shift)&3))  (0 outside)
+// so that for pixels stored XOR 0x80 (i.e. p - 128 as int8):
+//   2^21 + Σ p·k = bias + Σ_p 2^(8p) · Σ_j sdot4(pix4_j, Pp_j)   exactly.
+// Layout per axis: hdr[out][4] then planes[out][ngs][4] (ngs = stride).
+// ---------------------------------------------------------------------------
+namespace {
+
+inline void balanced_bytes(int32_t k, int8_t b[3]) {
+    int32_t r = k;
+    for (int p = 0; p < 3; ++p) {
+        int32_t lo = ((r + 128) & 255) - 128;
+        b[p] = (int8_t)lo;
+        r = (r - lo) >> 8;
+    }
+}
+
+}  // namespace
+
+extern "C" int32_t ipp_plan_dot4_stride(int32_t ksize) { return (ksize + 3 + 3) / 4; }
+
+extern "C" int64_t ipp_plan_dot4_size(int32_t out_size, int32_t ksize) {
+    return 4ll * out_size + 4ll * out_size * ipp_plan_dot4_stride(ksize);
+}
+
+// Convert standard Pillow taps (bounds[2*out] + taps[out*ksize]) into the dot4
+// format; `shift` is subtracted from every xmin (the V pass's ybox_first).
+extern "C" int ipp_plan_dot4_from_taps(int32_t out_size, int32_t ksize, const int32_t* std_taps, int32_t shift,
+                                       int32_t* out) {
+    if (out_size <= 0 || ksize <= 0 || !std_taps || !out) return IPP_E_ARG;
+    const int ngs = ipp_plan_dot4_stride(ksize);
+    const int32_t* bounds = std_taps;
+    const int32_t* kk = std_taps + 2 * (int64_t)out_size;
+    int32_t* hdr = out;
+    int32_t* planes = out + 4 * (int64_t)out_size;
+    for (int o = 0; o < out_size; ++o) {
+        const int xmin = bounds[2 * o] - shift, cnt = bounds[2 * o + 1];
+        if (xmin < 0) return IPP_E_RANGE;
+        const int off = xmin & 3, g0 = xmin - off;
+        const int ng = (off + cnt + 3) / 4;
+        if (ng > ngs) return IPP_E_RANGE;
+        int64_t sum = 0;
+        int32_t* pl = planes + (int64_t)o * ngs * 4;
+        for (int j = 0; j < ngs; ++j) pl[4 * j] = pl[4 * j + 1] = pl[4 * j + 2] = pl[4 * j + 3] = 0;
+        for (int t = 0; t < cnt; ++t) {
+            const int32_t k = kk[(int64_t)o * ksize + t];
+            sum += k;
+            int8_t b[3];
+            balanced_bytes(k, b);
+            const int pos = off + t, j = pos >> 2, bb = pos & 3;
+            for (int p = 0; p < 3; ++p)
+                pl[4 * j + p] |= (int32_t)((uint32_t)(uint8_t)b[p] << (8 * bb));
+        }
+        hdr[4 * o] = g0;
+        hdr[4 * o + 1] = ng;
+        hdr[4 * o + 2] = (int32_t)((1 << 21) + 128 * sum);
+        hdr[4 * o + 3] = 0;
+    }
+    return IPP_OK;
+}
+
+// Plan every axis of a pipe batch in the dot4 format.  Axis i resamples
+// in_sizes[i] → out_sizes[i]; identity[i] != 0 encodes "no pass on this axis"
+// (single 2^22 tap).  For axes with shift_first[i] != 0 the Pillow bounds are
+// shifted by their first xmin (ybox_first).  first_last[2i..2i+1] receives
+// (ybox_first, ybox_last) of the unshifted bounds.  offsets[i] = int32 offset
+// of the axis block in `out`, sized by ipp_plan_dot4_size(out, ksize(i)).
+extern "C" int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int32_t* out_sizes,
+                                  const int32_t* identity, const int32_t* shift_first, const int64_t* offsets,
+                                  int32_t* out, int32_t* first_last, int32_t n_threads) {
+    if (n < 0 || (n > 0 && (!in_sizes || !out_sizes || !identity || !shift_first || !offsets || !out || !first_last)))
+        return IPP_E_ARG;
+    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min(nt, 64));
+    if (n < 64) nt = 1;
+    std::vector<int> err(nt, 0);
+    auto work = [&](int t) {
+        std::vector<int32_t> tmp;
+        for (int i = t; i < n; i += nt) {
+            const int in = in_sizes[i], o = out_sizes[i];
+            int ksize;
+            if (identity[i]) {
+                ksize = 1;
+                tmp.assign(3 * (size_t)o, 0);
+                for (int x = 0; x < o; ++x) {
+                    tmp[2 * x] = x;
+                    tmp[2 * x + 1] = 1;
+                    tmp[2 * (size_t)o + x] = 1 << 22;
+                }
+            } else {
+                ksize = ipp_plan_lanczos_ksize(0.0, (double)in, o);
+                tmp.assign(2 * (size_t)o + (size_t)o * ksize, 0);
+                const int64_t r = ipp_plan_lanczos(in, 0.0, (double)in, o, tmp.data(), (int64_t)tmp.size());
+                if (r < 0) { err[t] = (int)r; continue; }
+            }
+            const int first = tmp[0], last = tmp[2 * (o - 1)] + tmp[2 * (o - 1) + 1];
+            first_last[2 * i] = first;
+            first_last[2 * i + 1] = last;
+            const int e = ipp_plan_dot4_from_taps(o, ksize, tmp.data(), shift_first[i] ? first : 0, out + offsets[i]);
+            if (e) err[t] = e;
+        }
+    };
+    if (nt == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
+        for (auto& x : th) x.join();
+    }
+    for (int e : err)
+        if (e) return e;
+    return IPP_OK;
+}

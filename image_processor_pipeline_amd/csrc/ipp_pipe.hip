@@ -6,57 +6,189 @@
 //
 // Stage chain of the reference (files between steps, one library pass per
 // op): recadrages.py:46 → rotations.py:55,96,99-101 → symmetry.py:114-119 →
-// filtres_liste.py:84-134 → overlays.py:129,138-139.  Here the RGBA cut-out
-// (the pipe image "M") is never materialised: the LANCZOS horizontal pass
-// computes each M pixel on the fly from the source (gather → HSV α →
-// premultiply) into an LDS window and runs the taps over it; the vertical pass
-// is fused with unpremultiply, the alpha blend and the background copy, so the
-// composite is written once with dwordx4 stores.
+// filtres_liste.py:84-134 → overlays.py:129,138-139.  The RGBA cut-out "M" is
+// never materialised: the LANCZOS horizontal pass computes each M pixel on the
+// fly from the source (gather → HSV α → premultiply) into a channel-planar
+// LDS window and runs the taps over it with v_dot4c_i32_i8; the vertical pass
+// is fused with unpremultiply, the alpha blend and the background copy.
 //
-// HBM traffic per image (algorithmic): source crop 3·Hc·Wc read, T (H-pass
-// output, 4·W'·rows) written + read, background 3·HW read, composite 3·HW
-// written.  See DESIGN.md §Kernels for the roofline accounting.
+// Exact integer arithmetic (Pillow Resample.c): each 22-bit tap k is split into
+// three balanced signed bytes (k = k0 + 256 k1 + 65536 k2) and every pixel p is
+// stored as p ^ 0x80 (= p - 128 as int8), so
+//   2^21 + Σ p·k = bias + Σ_b 2^(8b) Σ_j sdot4(p4_j, kb_j),  bias = 2^21 + 128 Σk
+// holds bit-for-bit (ipp_host.cpp ipp_plan_dot4_from_taps builds the planes).
+//
+// T (H-pass output) layout per item: [row group g][column x'][4 channels][4
+// rows] bytes (16 B per (g, x')), values XOR 0x80, so the V pass reads one
+// dwordx4 per 4 taps per pixel.  T rows are M rows [line0, line0 + lines).
 #include "ipp_hsv.h"
 
 namespace {
 
-constexpr int HX = 64;          // H-pass outputs per block (one per lane)
-constexpr int HR = 8;           // H-pass rows per block (2 per thread)
-constexpr int HWIN = 1024;      // LDS window width in pixels
-constexpr int VR = 4;           // composite rows per vblend block
+constexpr int HX = 64;            // H-pass outputs per block (one per lane)
+constexpr int HR = 16;            // H-pass rows per block (4 per thread)
+constexpr int WSTRIDE = 400;      // LDS bytes per plane row (≡ 4 dwords mod 32 banks)
+constexpr int NGL = 16;           // tap groups staged in LDS per output
+constexpr int VR = 4;             // composite rows per vblend block
 
-__device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c) { return __mul24(a, b) + c; }
-
-// Pixel (x, y) of the pipe image M, premultiplied (Convert.c rgbA2rgba): the
-// flipped, bbox-cropped, rotated crop with α replaced by the HSV keep mask.
-__device__ __forceinline__ uint32_t pipe_pixel(const uint8_t* __restrict__ src, const ipp_gather_desc& g,
-                                               const HsvLds& hs, int x, int y) {
-    const int fx = (g.flip & 1) ? g.out_w - 1 - x : x;
-    const int fy = (g.flip & 2) ? g.out_h - 1 - y : y;
-    const int X = g.off_x + fx, Y = g.off_y + fy;
-    const int32_t xx = (int32_t)((uint32_t)g.a2 + (uint32_t)Y * (uint32_t)g.a1 + (uint32_t)X * (uint32_t)g.a0);
-    const int32_t yy = (int32_t)((uint32_t)g.a5 + (uint32_t)Y * (uint32_t)g.a4 + (uint32_t)X * (uint32_t)g.a3);
-    const int xin = xx >> 16, yin = yy >> 16;
-    uint32_t px = 0u;
-    if ((unsigned)xin < (unsigned)g.in_w && (unsigned)yin < (unsigned)g.in_h) {
-        const int sx = g.in_x0 + xin, sy = g.in_y0 + yin;
-        const uint8_t* p = src + g.src_off + (int64_t)sy * g.src_pitch;
-        if (g.src_cn == 4) {
-            px = reinterpret_cast<const uint32_t*>(p)[sx];
-        } else {
-            const bool wide_ok = (sy < g.src_h - 1) || (sx < g.src_w - 1);
-            px = load_rgb_opaque(p + 3 * sx, wide_ok);
-        }
-    }
-    const uint32_t a = hsv_keep_alpha(hs, px, 0, x, y);
-    return premultiply((px & 0x00FFFFFFu) | (a << 24));
+__device__ __forceinline__ int32_t sdot4(uint32_t a, uint32_t b, int32_t c) {
+#ifdef IPP_DBG_NO_DOT4
+    int32_t s = c;
+    for (int i = 0; i < 4; ++i) s += (int32_t)(int8_t)(a >> (8 * i)) * (int32_t)(int8_t)(b >> (8 * i));
+    return s;
+#elif defined(IPP_DBG_VOP3P)
+    int32_t d;
+    asm("v_dot4_i32_i8 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+#else
+    return __builtin_amdgcn_sdot4((int32_t)a, (int32_t)b, c, false);
+#endif
 }
 
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// round(num / d) for d in [1, 255] and num < 2^21 whose quotient never lies
+// exactly on .5 (the OpenCV HSV table constants): float estimate, then an exact
+// integer ±1 correction.
+__device__ __forceinline__ int32_t round_div(float numf, int32_t num, int32_t d) {
+    d = d < 1 ? 1 : d;
+    const float q = numf * __builtin_amdgcn_rcpf((float)d);
+    int32_t qi = (int32_t)(q + 0.5f);
+    const int32_t r2 = 2 * (num - qi * d);
+    qi += (r2 > d) ? 1 : 0;
+    qi -= (r2 < -d) ? 1 : 0;
+    return qi;
+}
+
+// Per-block uniform HSV range state (SGPRs): bounds as (lo, hi - lo) for the
+// unsigned in-range trick, plus the zone rectangle resolved for this item.
+template <int NR>
+struct Ranges {
+    int32_t lo[NR][3], span[NR][3];
+    int32_t r0[NR], rh[NR], c0[NR], cw[NR];
+    uint32_t full[NR];  // bit c: channel c unconstrained; bit 3: zone = whole image
+};
+
+template <int NR>
+__device__ __forceinline__ void ranges_init(Ranges<NR>& R, const ipp_hsv_params& hp, int w, int h) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const ipp_hsv_range& q = hp.r[k];
+        uint32_t f = 0;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            R.lo[k][c] = q.lo[c];
+            R.span[k][c] = q.hi[c] - q.lo[c];
+            const int top = c == 0 ? 179 : 255;  // h < 180 for 8-bit HSV
+            if (q.lo[c] <= 0 && q.hi[c] >= top) f |= 1u << c;
+        }
+        int a, b, cc, dd;
+        slice_indices(q.zone[0], h - q.zone[1], h, a, b);
+        slice_indices(q.zone[2], w - q.zone[3], w, cc, dd);
+        R.r0[k] = a;
+        R.rh[k] = b - a;
+        R.c0[k] = cc;
+        R.cw[k] = dd - cc;
+        if (a == 0 && b == h && cc == 0 && dd == w) f |= 8u;
+        R.full[k] = f;
+    }
+}
+
+// OpenCV RGB2HSV_b (hsv_shift 12) + the union of inRange boxes → keep?
+template <int NR>
+__device__ __forceinline__ bool hsv_keep(const Ranges<NR>& R, uint32_t px, int x, int y) {
+    const int r = px & 0xFF, g = (px >> 8) & 0xFF, b = (px >> 16) & 0xFF;  // Pillow order
+    const int v = max(max(b, g), r);
+    const int vmin = min(min(b, g), r);
+    const int diff = v - vmin;
+    const int sdiv = round_div(1044480.0f, 1044480, v);   // cvRound((255 << 12) / v)
+    const int hdiv = round_div(122880.0f, 122880, diff);  // cvRound((180 << 12) / (6 diff))
+    const int sat = (diff * sdiv + (1 << 11)) >> 12;
+    int hh = (v == r) ? (g - b) : ((v == g) ? (b - r + 2 * diff) : (r - g + 4 * diff));
+    hh = (hh * hdiv + (1 << 11)) >> 12;
+    hh += hh < 0 ? 180 : 0;
+    bool excl = false;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        bool in = true;
+        if (!(R.full[k] & 1u)) in &= (uint32_t)(hh - R.lo[k][0]) <= (uint32_t)R.span[k][0];
+        if (!(R.full[k] & 2u)) in &= (uint32_t)(sat - R.lo[k][1]) <= (uint32_t)R.span[k][1];
+        if (!(R.full[k] & 4u)) in &= (uint32_t)(v - R.lo[k][2]) <= (uint32_t)R.span[k][2];
+        if (!(R.full[k] & 8u))
+            in &= ((uint32_t)(y - R.r0[k]) < (uint32_t)R.rh[k]) & ((uint32_t)(x - R.c0[k]) < (uint32_t)R.cw[k]);
+        excl |= in;
+    }
+    return !excl;
+}
+
+// Source sampling for M pixel (x, y): flip + bbox offset folded into the 16.16
+// map so xx = B2 + y*B1 + x*B0 (int32 wrap-around arithmetic, as Pillow).
+struct Sampler {
+    const uint8_t* base;  // source pixel (in_x0, in_y0)
+    uint32_t pitch, lim;  // lim: last byte offset from base where a dword load fits
+    int32_t b0, b1, b2, b3, b4, b5;
+    int32_t in_w, in_h, cn;
+};
+
+__device__ __forceinline__ Sampler make_sampler(const uint8_t* src, const ipp_gather_desc& g) {
+    Sampler s;
+    s.base = src + g.src_off + (int64_t)g.in_y0 * g.src_pitch + (int64_t)g.in_x0 * g.src_cn;
+    s.pitch = (uint32_t)g.src_pitch;
+    const int64_t avail = (int64_t)(g.src_h - g.in_y0) * g.src_pitch - (int64_t)g.in_x0 * g.src_cn;
+    s.lim = (uint32_t)(avail - 4);
+    const int sgx = (g.flip & 1) ? -1 : 1, sgy = (g.flip & 2) ? -1 : 1;
+    const uint32_t sx0 = (uint32_t)(g.off_x + ((g.flip & 1) ? g.out_w - 1 : 0));
+    const uint32_t sy0 = (uint32_t)(g.off_y + ((g.flip & 2) ? g.out_h - 1 : 0));
+    s.b0 = (int32_t)((uint32_t)sgx * (uint32_t)g.a0);
+    s.b1 = (int32_t)((uint32_t)sgy * (uint32_t)g.a1);
+    s.b2 = (int32_t)((uint32_t)g.a2 + sy0 * (uint32_t)g.a1 + sx0 * (uint32_t)g.a0);
+    s.b3 = (int32_t)((uint32_t)sgx * (uint32_t)g.a3);
+    s.b4 = (int32_t)((uint32_t)sgy * (uint32_t)g.a4);
+    s.b5 = (int32_t)((uint32_t)g.a5 + sy0 * (uint32_t)g.a4 + sx0 * (uint32_t)g.a3);
+    s.in_w = g.in_w;
+    s.in_h = g.in_h;
+    s.cn = g.src_cn;
+    return s;
+}
+
+// Load the source pixel for (xx, yy) in 16.16, or 0 outside (Pillow fill).
+__device__ __forceinline__ uint32_t sample(const Sampler& s, int32_t xx, int32_t yy, bool& valid) {
+    const int xin = xx >> 16, yin = yy >> 16;
+    valid = ((uint32_t)xin < (uint32_t)s.in_w) & ((uint32_t)yin < (uint32_t)s.in_h);
+    if (!valid) return 0u;
+    const uint32_t off = (uint32_t)yin * s.pitch + (uint32_t)(xin * s.cn);
+    if (s.cn == 4) return *reinterpret_cast<const uint32_t*>(s.base + off);
+    const uint32_t d = off > s.lim ? 1u : 0u;  // last pixel of the buffer: shift a dword window
+    return (ld_u32_unaligned(s.base + off - d) >> (8 * d)) | 0xFF000000u;
+}
+
+// Transpose 4 packed pixels (RGBA each) into 4 channel-planar dwords.
+__device__ __forceinline__ void transpose4(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, uint32_t ch[4]) {
+    const uint32_t lo01 = perm(p1, p0, 0x05010400u), hi01 = perm(p1, p0, 0x07030602u);
+    const uint32_t lo23 = perm(p3, p2, 0x05010400u), hi23 = perm(p3, p2, 0x07030602u);
+    ch[0] = perm(lo23, lo01, 0x05040100u);
+    ch[1] = perm(lo23, lo01, 0x07060302u);
+    ch[2] = perm(hi23, hi01, 0x05040100u);
+    ch[3] = perm(hi23, hi01, 0x07060302u);
+}
+
+#ifdef IPP_DBG_DUMP
+__device__ uint8_t g_dbg_win[4 * 16 * 400];
+__device__ int32_t g_dbg_meta[8];
+#endif
+
+struct HpassLds {
+    uint8_t win[4][HR][WSTRIDE];      // planar window, bytes p ^ 0x80
+    uint4 taps[NGL][HX];              // tap planes (P0, P1, P2, -) per group, per output
+};
+
+template <int NR>
 __global__ void __launch_bounds__(256)
 k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
              const ipp_pipe_desc* __restrict__ descs, int tiles_x, int tiles_y, ipp_hsv_params hp) {
-    __shared__ HsvLds hs;
-    __shared__ uint32_t win[HR][HWIN];
+    __shared__ HpassLds L;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int per_img = tiles_x * tiles_y;
     const int im = b / per_img;
@@ -66,50 +198,141 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
     const ipp_resample_desc h = descs[im].h;
     const int xo0 = tx * HX, row0 = ty * HR;
     if (xo0 >= h.out_len || row0 >= h.lines) return;  // block-uniform
-    hsv_lds_init(hs, hp, g.out_w, g.out_h);
-    const int32_t* bnd = coefs + h.coef_off;
-    const int32_t* taps = bnd + 2 * h.out_len;
-    const int xo_end = min(xo0 + HX, h.out_len);
-    const int lane = threadIdx.x & 63, rsub = threadIdx.x >> 6;  // rsub in [0,4)
-    const int nrows = min(HR, h.lines - row0);
-    __syncthreads();
 
-    // Sub-chunks of outputs whose input window fits the LDS window.
+    Ranges<NR> R;
+    ranges_init<NR>(R, hp, g.out_w, g.out_h);
+    const Sampler S = make_sampler(src, g);
+    const int ngs = h.ksize;  // tap-group stride of this item (dot4 format)
+    const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
+    const uint4* planes = reinterpret_cast<const uint4*>(coefs + h.coef_off + 4 * (int64_t)h.out_len);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nrows = min(HR, h.lines - row0);
+    const bool taps_in_lds = ngs <= NGL;
+
+    // Outputs of this block: split into sub-chunks whose window fits WSTRIDE.
+    const int xo_end = min(xo0 + HX, h.out_len);
     for (int s0 = xo0; s0 < xo_end;) {
         int s1 = xo_end;
-        while (s1 - s0 > 1 && bnd[2 * (s1 - 1)] + bnd[2 * (s1 - 1) + 1] - bnd[2 * s0] > HWIN)
-            s1 = s0 + (s1 - s0 + 1) / 2;
-        const int wlo = bnd[2 * s0];
-        const int ww = bnd[2 * (s1 - 1)] + bnd[2 * (s1 - 1) + 1] - wlo;
-        for (int i = threadIdx.x; i < nrows * ww; i += 256) {
-            const int r = i / ww, c = i - r * ww;
-            win[r][c] = pipe_pixel(src, g, hs, wlo + c, h.line0 + row0 + r);
+        while (s1 - s0 > 1 && hdr[s1 - 1].x + 4 * ngs - hdr[s0].x > WSTRIDE) s1 = s0 + (s1 - s0 + 1) / 2;
+        const int W0 = hdr[s0].x;
+        const int ww = hdr[s1 - 1].x + 4 * ngs - W0;  // multiple of 4
+        const int ng4 = ww >> 2;
+
+        // Phase 0: stage tap planes (transposed: [group][output]).
+        if (taps_in_lds) {
+            for (int i = threadIdx.x; i < ngs * HX; i += 256) {
+                const int j = i / HX, o = i - j * HX;
+                L.taps[j][o] = (s0 + o < s1) ? planes[(int64_t)(s0 + o) * ngs + j] : make_uint4(0, 0, 0, 0);
+            }
+        }
+
+        // Phase 1: M pixels of the window → planar LDS (16 rows × 16 px per wave step).
+        const int r = lane >> 2;
+        const int y = h.line0 + row0 + r;
+        const uint32_t rowx = (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1;
+        const uint32_t rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
+        for (int cg0 = wave * 4; cg0 < ng4; cg0 += 16) {
+            const int cg = cg0 + (lane & 3);
+            const int x = W0 + 4 * cg;
+            uint32_t px[4];
+            bool vany = false;
+            uint32_t xx = rowx + (uint32_t)x * (uint32_t)S.b0, yy = rowy + (uint32_t)x * (uint32_t)S.b3;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                bool valid;
+                px[k] = sample(S, (int32_t)xx, (int32_t)yy, valid);
+                vany |= valid;
+                xx += (uint32_t)S.b0;
+                yy += (uint32_t)S.b3;
+            }
+            const bool active = (cg < ng4) && (r < nrows);
+            // waves whose 64 pixels all fall outside the source: every M value
+            // is the (per-item constant) transparent fill — no HSV work.
+            if (__ballot(vany && active) != 0ull) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const bool keep = hsv_keep<NR>(R, px[k], x + k, y);
+                    px[k] = keep ? (px[k] | 0xFF000000u) : 0u;  // premultiplied, α ∈ {0, 255}
+                }
+            } else {
+                // all-fill wave: HSV of black is constant, only zones vary
+#pragma unroll
+                for (int k = 0; k < 4; ++k) px[k] = hsv_keep<NR>(R, 0u, x + k, y) ? 0xFF000000u : 0u;
+            }
+            if (active) {
+                uint32_t ch[4];
+                transpose4(px[0], px[1], px[2], px[3], ch);
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    *reinterpret_cast<uint32_t*>(&L.win[c][r][4 * cg]) = ch[c] ^ 0x80808080u;
+            }
         }
         __syncthreads();
+#ifdef IPP_DBG_DUMP
+        if (im == 0 && tx == 0 && ty == 0 && s0 == xo0) {
+            for (int i = threadIdx.x; i < 4 * HR * WSTRIDE; i += 256) g_dbg_win[i] = (&L.win[0][0][0])[i];
+            if (threadIdx.x == 0) { g_dbg_meta[0] = W0; g_dbg_meta[1] = ww; g_dbg_meta[2] = ngs; g_dbg_meta[3] = s1; }
+        }
+#endif
+
+        // Phase 2: output x' = s0 + lane, rows 4*wave .. 4*wave+3.
         const int xo = s0 + lane;
         if (xo < s1) {
-            const int xmin = bnd[2 * xo] - wlo, cnt = bnd[2 * xo + 1];
-            const int32_t* kk = taps + (int64_t)xo * h.ksize;
-            for (int r = rsub; r < nrows; r += 4) {
-                int32_t a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21, a3 = 1 << 21;
-                const uint32_t* w = &win[r][xmin];
-                for (int k = 0; k < cnt; ++k) {
-                    const uint32_t p = w[k];
-                    const int32_t c = kk[k];
-                    a0 = mad24((int32_t)(p & 0xFF), c, a0);
-                    a1 = mad24((int32_t)((p >> 8) & 0xFF), c, a1);
-                    a2 = mad24((int32_t)((p >> 16) & 0xFF), c, a2);
-                    a3 = mad24((int32_t)(p >> 24), c, a3);
+            const int4 hd = hdr[xo];
+            const int wo = hd.x - W0;
+            int32_t acc[4][4][3];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[rr][c][0] = acc[rr][c][1] = acc[rr][c][2] = 0;
+            for (int j = 0; j < ngs; ++j) {
+                const uint4 tp = taps_in_lds ? L.taps[j][lane] : planes[(int64_t)xo * ngs + j];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int row = 4 * wave + rr;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const uint32_t w = *reinterpret_cast<const uint32_t*>(&L.win[c][row][wo + 4 * j]);
+                        acc[rr][c][0] = sdot4(w, tp.x, acc[rr][c][0]);
+                        acc[rr][c][1] = sdot4(w, tp.y, acc[rr][c][1]);
+                        acc[rr][c][2] = sdot4(w, tp.z, acc[rr][c][2]);
+                    }
                 }
-                const uint32_t o = clip8(a0) | (clip8(a1) << 8) | (clip8(a2) << 16) | (clip8(a3) << 24);
-                reinterpret_cast<uint32_t*>(tmp + h.dst_off + (int64_t)(row0 + r) * h.dst_pitch)[xo] = o;
             }
+            uint32_t outc[4] = {0u, 0u, 0u, 0u};
+#ifdef IPP_DBG_WIN
+            // debug: T <- raw window pixel at column g0(x') (premultiplied M)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    acc[rr][c][0] = (int32_t)((L.win[c][4 * wave + rr][wo] ^ 0x80u)) << 22, acc[rr][c][1] = 0,
+                    acc[rr][c][2] = 0;
+            const int4 hd0 = make_int4(hd.x, hd.y, 1 << 21, 0);
+#define hd hd0
+#endif
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int32_t ss = hd.z + acc[rr][c][0] + (acc[rr][c][1] << 8) + (acc[rr][c][2] << 16);
+                    outc[c] |= clip8(ss) << (8 * rr);
+                }
+#ifdef IPP_DBG_WIN
+#undef hd
+#endif
+            const int grp = (row0 >> 2) + wave;
+            uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
+            *dst = make_uint4(outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
+                              outc[3] ^ 0x80808080u);
         }
         __syncthreads();
         s0 = s1;
     }
 }
 
+// V pass over T (dot4) → unpremultiply → blend onto the background, fused with
+// the background copy.  Block = VR composite rows.
 __global__ void __launch_bounds__(256)
 k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
               const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int tiles_y, int bg_w_max) {
@@ -118,35 +341,44 @@ k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, u
     const int im = b / tiles_y;
     const int ty = b - im * tiles_y;
     const ipp_resample_desc v = descs[im].v;
-    const ipp_resample_desc h = descs[im].h;
     const ipp_paste_desc p = descs[im].p;
     const int y0 = ty * VR;
     if (y0 >= p.bg_h) return;
     const int nrows = min(VR, p.bg_h - y0);
 
-    // Phase 1: overlay rows of this band — V pass over T, unpremultiply.
-    const int32_t* bnd = coefs + v.coef_off;
-    const int32_t* taps = bnd + 2 * v.out_len;
+    // Phase 1: overlay rows of this band.
+    const int ngs = v.ksize;
+    const int4* hdr = reinterpret_cast<const int4*>(coefs + v.coef_off);
+    const uint4* planes = reinterpret_cast<const uint4*>(coefs + v.coef_off + 4 * (int64_t)v.out_len);
     bool any = false;
     for (int r = 0; r < nrows; ++r) {
         const int oy = y0 + r - p.y;
         if ((unsigned)oy >= (unsigned)p.ov_h) continue;
         any = true;
-        const int ymin = bnd[2 * oy], cnt = bnd[2 * oy + 1];
-        const int32_t* kk = taps + (int64_t)oy * v.ksize;
+        const int4 hd = hdr[oy];
+        const uint4* tp = planes + (int64_t)oy * ngs;
+        const uint4* col0 = reinterpret_cast<const uint4*>(tmp + v.src_off + (int64_t)(hd.x >> 2) * v.src_pitch);
+        const int gstride = v.src_pitch >> 4;
         for (int x = threadIdx.x; x < p.ov_w; x += 256) {
-            const uint8_t* col = tmp + h.dst_off + (int64_t)ymin * h.dst_pitch + 4 * (int64_t)x;
-            int32_t a0 = 1 << 21, a1 = 1 << 21, a2 = 1 << 21, a3 = 1 << 21;
-            for (int k = 0; k < cnt; ++k) {
-                const uint32_t q = *reinterpret_cast<const uint32_t*>(col + (int64_t)k * h.dst_pitch);
-                const int32_t c = kk[k];
-                a0 = mad24((int32_t)(q & 0xFF), c, a0);
-                a1 = mad24((int32_t)((q >> 8) & 0xFF), c, a1);
-                a2 = mad24((int32_t)((q >> 16) & 0xFF), c, a2);
-                a3 = mad24((int32_t)(q >> 24), c, a3);
+            int32_t acc[4][3];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c][0] = acc[c][1] = acc[c][2] = 0;
+            const uint4* q = col0 + x;
+            for (int j = 0; j < ngs; ++j) {
+                const uint4 w = q[(int64_t)j * gstride];
+                const uint4 k = tp[j];
+                const uint32_t wc[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    acc[c][0] = sdot4(wc[c], k.x, acc[c][0]);
+                    acc[c][1] = sdot4(wc[c], k.y, acc[c][1]);
+                    acc[c][2] = sdot4(wc[c], k.z, acc[c][2]);
+                }
             }
-            orow[r * bg_w_max + x] =
-                unpremultiply(clip8(a0) | (clip8(a1) << 8) | (clip8(a2) << 16) | (clip8(a3) << 24));
+            uint32_t o = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) o |= clip8(hd.z + acc[c][0] + (acc[c][1] << 8) + (acc[c][2] << 16)) << (8 * c);
+            orow[r * bg_w_max + x] = unpremultiply(o);
         }
     }
     if (any) __syncthreads();
@@ -154,54 +386,85 @@ k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, u
     // Phase 2: composite rows = background bytes, blended inside the footprint.
     const int row_bytes = 3 * p.bg_w;
     const int chunks = (row_bytes + 15) >> 4;
-    for (int i = threadIdx.x; i < nrows * chunks; i += 256) {
-        const int r = i / chunks, c0 = (i - r * chunks) << 4;
+    for (int r = 0; r < nrows; ++r) {
         const int y = y0 + r;
         const uint8_t* brow = bg + p.bg_off + (int64_t)y * p.bg_pitch;
         uint8_t* drow = dst + p.dst_off + (int64_t)y * p.dst_pitch;
-        const int nbytes = min(16, row_bytes - c0);
-        const bool vec = nbytes == 16 &&
-                         ((reinterpret_cast<uintptr_t>(brow + c0) | reinterpret_cast<uintptr_t>(drow + c0)) & 15u) == 0;
-        uint8_t vb[16];
-        if (vec) {
-            *reinterpret_cast<uint4*>(vb) = *reinterpret_cast<const uint4*>(brow + c0);
-        } else {
-            for (int j = 0; j < nbytes; ++j) vb[j] = brow[c0 + j];
-        }
         const int oy = y - p.y;
-        if ((unsigned)oy < (unsigned)p.ov_h && c0 + nbytes > 3 * p.x && c0 < 3 * (p.x + p.ov_w)) {
-            int px = c0 / 3, ch = c0 - 3 * px;
-            for (int j = 0; j < nbytes; ++j) {
-                const int ox = px - p.x;
-                if ((unsigned)ox < (unsigned)p.ov_w) {
-                    const uint32_t o = orow[r * bg_w_max + ox];
-                    const uint32_t a = o >> 24;
-                    vb[j] = (uint8_t)div255((uint32_t)vb[j] * (255u - a) + ((o >> (8 * ch)) & 0xFFu) * a);
-                }
-                if (++ch == 3) { ch = 0; ++px; }
+        const bool in_rows = (unsigned)oy < (unsigned)p.ov_h;
+        for (int ci = threadIdx.x; ci < chunks; ci += 256) {
+            const int c0 = ci << 4;
+            const int nbytes = min(16, row_bytes - c0);
+            const bool vec = nbytes == 16 &&
+                             ((reinterpret_cast<uintptr_t>(brow + c0) | reinterpret_cast<uintptr_t>(drow + c0)) & 15u) == 0;
+            uint8_t vb[16];
+            if (vec) {
+                *reinterpret_cast<uint4*>(vb) = *reinterpret_cast<const uint4*>(brow + c0);
+            } else {
+                for (int j = 0; j < nbytes; ++j) vb[j] = brow[c0 + j];
             }
-        }
-        if (vec) {
-            *reinterpret_cast<uint4*>(drow + c0) = *reinterpret_cast<const uint4*>(vb);
-        } else {
-            for (int j = 0; j < nbytes; ++j) drow[c0 + j] = vb[j];
+            if (in_rows && c0 + nbytes > 3 * p.x && c0 < 3 * (p.x + p.ov_w)) {
+                int px = c0 / 3, ch = c0 - 3 * px;
+                for (int j = 0; j < nbytes; ++j) {
+                    const int ox = px - p.x;
+                    if ((unsigned)ox < (unsigned)p.ov_w) {
+                        const uint32_t o = orow[r * bg_w_max + ox];
+                        const uint32_t a = o >> 24;
+                        vb[j] = (uint8_t)div255((uint32_t)vb[j] * (255u - a) + ((o >> (8 * ch)) & 0xFFu) * a);
+                    }
+                    if (++ch == 3) { ch = 0; ++px; }
+                }
+            }
+            if (vec) {
+                *reinterpret_cast<uint4*>(drow + c0) = *reinterpret_cast<const uint4*>(vb);
+            } else {
+                for (int j = 0; j < nbytes; ++j) drow[c0 + j] = vb[j];
+            }
         }
     }
 }
 
+template <int NR>
+void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
+                  const ipp_pipe_desc* descs, int tx, int ty, const ipp_hsv_params& hp) {
+    hipLaunchKernelGGL(k_pipe_hpass<NR>, grid, dim3(256), 0, s, src, tmp, coefs, descs, tx, ty, hp);
+}
+
 }  // namespace
+
+#ifdef IPP_DBG_DUMP
+extern "C" int ipp_dbg_dump(void* win, void* meta) {
+    hipMemcpyFromSymbol(win, HIP_SYMBOL(g_dbg_win), sizeof(g_dbg_win));
+    hipMemcpyFromSymbol(meta, HIP_SYMBOL(g_dbg_meta), sizeof(g_dbg_meta));
+    return 0;
+}
+#endif
 
 extern "C" int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
                               int32_t n_images, int32_t max_out_w, int32_t max_rows, const ipp_hsv_params* hsv,
                               void* stream) {
     if (n_images == 0) return IPP_OK;
     if (!src || !tmp || !coefs || !descs || !hsv || n_images < 0 || max_out_w <= 0 || max_rows <= 0) return IPP_E_ARG;
-    if (hsv->n_ranges < 0 || hsv->n_ranges > IPP_MAX_HSV_RANGES) return IPP_E_ARG;
     const int tx = (max_out_w + HX - 1) / HX, ty = (max_rows + HR - 1) / HR;
     const int64_t blocks = (int64_t)tx * ty * n_images;
     if (blocks >= INT32_MAX) return IPP_E_ARG;
-    hipLaunchKernelGGL(k_pipe_hpass, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, src, tmp, coefs,
-                       descs, tx, ty, *hsv);
+    const dim3 grid((uint32_t)blocks);
+    hipStream_t s = (hipStream_t)stream;
+    switch (hsv->n_ranges) {
+        case 0: launch_hpass<0>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 1: launch_hpass<1>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 2: launch_hpass<2>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 3: launch_hpass<3>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 4: launch_hpass<4>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 5: launch_hpass<5>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 6: launch_hpass<6>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 7: launch_hpass<7>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 8: launch_hpass<8>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        default:
+            if (hsv->n_ranges > IPP_MAX_HSV_RANGES) return IPP_E_ARG;
+            launch_hpass<IPP_MAX_HSV_RANGES>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv);
+            break;
+    }
     IPP_CHECK_LAUNCH();
     return IPP_OK;
 }

@@ -134,29 +134,24 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
         axes_in += [rw, rh]
         axes_out += [nw_, nh_]
 
-    # ---- taps (C planner, threaded) -------------------------------------
+    # ---- taps (C planner, threaded; dot4 format, see ipp_host.cpp) --------
     lib = N.load()
-    sizes = np.zeros(2 * n, np.int64)
-    ks = np.zeros(2 * n, np.int64)
-    for j in range(2 * n):
-        idn = identity[j // 2][j % 2]
-        k = 1 if idn else lib.ipp_plan_lanczos_ksize(0.0, float(axes_in[j]), axes_out[j])
-        ks[j] = k
-        sizes[j] = 2 * axes_out[j] + axes_out[j] * k
-    offs = np.zeros(2 * n, np.int64)
+    m = 2 * n
+    a_in = np.asarray(axes_in, np.int32)
+    a_out = np.asarray(axes_out, np.int32)
+    ident = np.array([identity[j // 2][j % 2] for j in range(m)], np.int32)
+    # V axes are shifted to ybox_first whenever Pillow runs the H pass
+    shift = np.array([(j % 2 == 1) and not identity[j // 2][0] for j in range(m)], np.int32)
+    ks = np.array([1 if ident[j] else lib.ipp_plan_lanczos_ksize(0.0, float(a_in[j]), int(a_out[j]))
+                   for j in range(m)], np.int64)
+    ngs = np.array([lib.ipp_plan_dot4_stride(int(k)) for k in ks], np.int64)
+    sizes = 4 * a_out.astype(np.int64) * (1 + ngs)
+    offs = np.zeros(m, np.int64)
     offs[1:] = np.cumsum(sizes)[:-1]
     coefs = np.zeros(int(sizes.sum()), np.int32)
-    sel = np.array([not identity[j // 2][j % 2] for j in range(2 * n)])
-    idx = np.flatnonzero(sel)
-    if idx.size:
-        ins = np.array([axes_in[j] for j in idx], np.int32)
-        outs = np.array([axes_out[j] for j in idx], np.int32)
-        o = offs[idx].astype(np.int64)
-        N.check(lib.ipp_plan_lanczos_batch(len(idx), N.np_ptr(ins), N.np_ptr(outs), N.np_ptr(o), N.np_ptr(coefs),
-                                           coefs.size, 0), "ipp_plan_lanczos_batch")
-    for j in np.flatnonzero(~sel):
-        _, buf = G.identity_taps(axes_out[j])
-        coefs[offs[j]:offs[j] + buf.size] = buf
+    first_last = np.zeros(2 * m, np.int32)
+    N.check(lib.ipp_plan_pipe_axes(m, N.np_ptr(a_in), N.np_ptr(a_out), N.np_ptr(ident), N.np_ptr(shift),
+                                   N.np_ptr(offs), N.np_ptr(coefs), N.np_ptr(first_last), 0), "ipp_plan_pipe_axes")
 
     # ---- descriptors ----------------------------------------------------
     tmp_off = 0
@@ -166,24 +161,22 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
         rh, rw = cut_dims[i]
         nh_, nw_ = ov_dims[i]
         jh, jv = 2 * i, 2 * i + 1
-        vb = coefs[offs[jv]:offs[jv] + 2 * nh_]
-        need_h = not identity[i][0]
-        if need_h:
-            y0 = int(vb[0])
-            y1 = int(vb[2 * nh_ - 2] + vb[2 * nh_ - 1])
-            vb[0::2] -= y0
+        if not identity[i][0]:
+            y0, y1 = int(first_last[2 * jv]), int(first_last[2 * jv + 1])
         else:
             y0, y1 = 0, rh
         rows = y1 - y0
+        groups = ((rows + 15) // 16) * 4 + int(ngs[jv]) + 1   # + V-pass over-read pad
+        pitch = 16 * nw_
         h = d[i]["h"]
         h["dst_off"] = tmp_off
-        h["dst_pitch"] = 4 * nw_
-        h["in_len"], h["out_len"], h["lines"], h["line0"], h["ksize"] = rw, nw_, rows, y0, ks[jh]
+        h["dst_pitch"] = pitch
+        h["in_len"], h["out_len"], h["lines"], h["line0"], h["ksize"] = rw, nw_, rows, y0, ngs[jh]
         h["coef_off"] = offs[jh]
         v = d[i]["v"]
         v["src_off"] = tmp_off
-        v["src_pitch"] = 4 * nw_
-        v["in_len"], v["out_len"], v["lines"], v["ksize"] = rows, nh_, nw_, ks[jv]
+        v["src_pitch"] = pitch
+        v["in_len"], v["out_len"], v["lines"], v["ksize"] = rows, nh_, nw_, ngs[jv]
         v["coef_off"] = offs[jv]
         p = d[i]["p"]
         it = params[i]
@@ -191,12 +184,13 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
         p["dst_off"] = i * bh * bw * 3
         p["bg_w"], p["bg_h"], p["bg_pitch"], p["dst_pitch"] = bw, bh, 3 * bw, 3 * bw
         p["ov_w"], p["ov_h"], p["ov_pitch"], p["x"], p["y"] = nw_, nh_, 4 * nw_, it.x, it.y
-        tmp_off += 4 * nw_ * rows
+        tmp_off += pitch * groups
         tmp_off = (tmp_off + 255) // 256 * 256
         max_out_w = max(max_out_w, nw_)
         max_rows = max(max_rows, rows)
-        algo_h += 3 * hc * wc + 4 * nw_ * rows
-        algo_v += 4 * nw_ * rows + 3 * bh * bw + 3 * bh * bw
+        t_bytes = pitch * ((rows + 3) // 4)
+        algo_h += 3 * hc * wc + t_bytes
+        algo_v += t_bytes + 3 * bh * bw + 3 * bh * bw
     hsv = G.hsv_params(cfg.hsv_ranges, cfg.zones, cfg.use_gimp_scale, bgr=False)
     return PipePlan(d, coefs, hsv, params, cut_dims, ov_dims, max(tmp_off, 256), max_out_w, max_rows, bw, bh,
                     algo_h, algo_v)

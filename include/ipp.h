@@ -216,6 +216,20 @@ int64_t ipp_plan_lanczos(int32_t in_size, double in0, double in1, int32_t out_si
 int ipp_plan_lanczos_batch(int32_t n, const int32_t* in_sizes, const int32_t* out_sizes,
                            const int64_t* offsets, int32_t* out, int64_t out_capacity,
                            int32_t n_threads);
+/* dot4 tap format of the fused pipe kernels (see ipp_host.cpp): per output
+ * hdr (g0, ng, bias, 0) then ng tap groups of 3 balanced signed byte planes;
+ * stride = groups reserved per output; size = int32 count for an axis. */
+int32_t ipp_plan_dot4_stride(int32_t ksize);
+int64_t ipp_plan_dot4_size(int32_t out_size, int32_t ksize);
+int ipp_plan_dot4_from_taps(int32_t out_size, int32_t ksize, const int32_t* std_taps,
+                            int32_t shift, int32_t* out);
+/* Plan every axis of a pipe batch in the dot4 format (threaded); identity[i]
+ * = no pass on that axis; shift_first[i] = shift bounds to ybox_first;
+ * first_last receives (ybox_first, ybox_last) per axis. */
+int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int32_t* out_sizes,
+                       const int32_t* identity, const int32_t* shift_first,
+                       const int64_t* offsets, int32_t* out, int32_t* first_last,
+                       int32_t n_threads);
 /* ksize for (in_size, out_size) without computing taps. */
 int32_t ipp_plan_lanczos_ksize(double in0, double in1, int32_t out_size);
 
