@@ -81,7 +81,7 @@ SIGNATURES = {
     "ipp_lanczos_h": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ipp_lanczos_v": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ipp_paste_blend": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
-    "ipp_pipe_hpass": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "ipp_pipe_hpass": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "ipp_pipe_vblend": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "ipp_ccl_keep_largest": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "ipp_alpha_bbox": (_I, [_P, _P, _I, _I, _I, _P, _P]),

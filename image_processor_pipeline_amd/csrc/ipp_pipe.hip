@@ -49,75 +49,62 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
-// round(num / d) for d in [1, 255] and num < 2^21 whose quotient never lies
-// exactly on .5 (the OpenCV HSV table constants): float estimate, then an exact
-// integer ±1 correction.
-__device__ __forceinline__ int32_t round_div(float numf, int32_t num, int32_t d) {
-    d = d < 1 ? 1 : d;
-    const float q = numf * __builtin_amdgcn_rcpf((float)d);
-    int32_t qi = (int32_t)(q + 0.5f);
-    const int32_t r2 = 2 * (num - qi * d);
-    qi += (r2 > d) ? 1 : 0;
-    qi -= (r2 < -d) ? 1 : 0;
-    return qi;
-}
+// Per-block uniform HSV range state (SGPRs).  h and s are tested together as
+// packed 16-bit lanes: d = (h,s) - lo (wrapping), in range ⟺ min(d, span) == d.
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
-// Per-block uniform HSV range state (SGPRs): bounds as (lo, hi - lo) for the
-// unsigned in-range trick, plus the zone rectangle resolved for this item.
+__device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us2, v); }
+
 template <int NR>
 struct Ranges {
-    int32_t lo[NR][3], span[NR][3];
+    uint32_t lohs[NR], sphs[NR];   // (lo_h | lo_s << 16), (span_h | span_s << 16)
+    int32_t lov[NR], spv[NR];
     int32_t r0[NR], rh[NR], c0[NR], cw[NR];
-    uint32_t full[NR];  // bit c: channel c unconstrained; bit 3: zone = whole image
 };
 
-template <int NR>
+template <int NR, bool ZONES>
 __device__ __forceinline__ void ranges_init(Ranges<NR>& R, const ipp_hsv_params& hp, int w, int h) {
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
         const ipp_hsv_range& q = hp.r[k];
-        uint32_t f = 0;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            R.lo[k][c] = q.lo[c];
-            R.span[k][c] = q.hi[c] - q.lo[c];
-            const int top = c == 0 ? 179 : 255;  // h < 180 for 8-bit HSV
-            if (q.lo[c] <= 0 && q.hi[c] >= top) f |= 1u << c;
+        R.lohs[k] = (uint32_t)q.lo[0] | ((uint32_t)q.lo[1] << 16);
+        R.sphs[k] = (uint32_t)(q.hi[0] - q.lo[0]) | ((uint32_t)(q.hi[1] - q.lo[1]) << 16);
+        R.lov[k] = q.lo[2];
+        R.spv[k] = q.hi[2] - q.lo[2];
+        if (ZONES) {
+            int a, b, cc, dd;
+            slice_indices(q.zone[0], h - q.zone[1], h, a, b);
+            slice_indices(q.zone[2], w - q.zone[3], w, cc, dd);
+            R.r0[k] = a;
+            R.rh[k] = b - a;
+            R.c0[k] = cc;
+            R.cw[k] = dd - cc;
         }
-        int a, b, cc, dd;
-        slice_indices(q.zone[0], h - q.zone[1], h, a, b);
-        slice_indices(q.zone[2], w - q.zone[3], w, cc, dd);
-        R.r0[k] = a;
-        R.rh[k] = b - a;
-        R.c0[k] = cc;
-        R.cw[k] = dd - cc;
-        if (a == 0 && b == h && cc == 0 && dd == w) f |= 8u;
-        R.full[k] = f;
     }
 }
 
-// OpenCV RGB2HSV_b (hsv_shift 12) + the union of inRange boxes → keep?
-template <int NR>
-__device__ __forceinline__ bool hsv_keep(const Ranges<NR>& R, uint32_t px, int x, int y) {
+// OpenCV RGB2HSV_b (hsv_shift 12; sdiv/hdiv tables in LDS) + the union of
+// inRange boxes (and zones) → keep?
+template <int NR, bool ZONES>
+__device__ __forceinline__ bool hsv_keep(const Ranges<NR>& R, const int32_t* sdiv_t, const int32_t* hdiv_t,
+                                         uint32_t px, int x, int y) {
     const int r = px & 0xFF, g = (px >> 8) & 0xFF, b = (px >> 16) & 0xFF;  // Pillow order
     const int v = max(max(b, g), r);
     const int vmin = min(min(b, g), r);
     const int diff = v - vmin;
-    const int sdiv = round_div(1044480.0f, 1044480, v);   // cvRound((255 << 12) / v)
-    const int hdiv = round_div(122880.0f, 122880, diff);  // cvRound((180 << 12) / (6 diff))
-    const int sat = (diff * sdiv + (1 << 11)) >> 12;
+    const int sat = (int)(((uint32_t)__umul24(diff, sdiv_t[v]) + 2048u) >> 12);
     int hh = (v == r) ? (g - b) : ((v == g) ? (b - r + 2 * diff) : (r - g + 4 * diff));
-    hh = (hh * hdiv + (1 << 11)) >> 12;
+    hh = (__mul24(hh, hdiv_t[diff]) + 2048) >> 12;
     hh += hh < 0 ? 180 : 0;
+    const us2 hs = as_us2((uint32_t)hh | ((uint32_t)sat << 16));
     bool excl = false;
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
-        bool in = true;
-        if (!(R.full[k] & 1u)) in &= (uint32_t)(hh - R.lo[k][0]) <= (uint32_t)R.span[k][0];
-        if (!(R.full[k] & 2u)) in &= (uint32_t)(sat - R.lo[k][1]) <= (uint32_t)R.span[k][1];
-        if (!(R.full[k] & 4u)) in &= (uint32_t)(v - R.lo[k][2]) <= (uint32_t)R.span[k][2];
-        if (!(R.full[k] & 8u))
-            in &= ((uint32_t)(y - R.r0[k]) < (uint32_t)R.rh[k]) & ((uint32_t)(x - R.c0[k]) < (uint32_t)R.cw[k]);
+        const us2 d = hs - as_us2(R.lohs[k]);
+        const us2 m = __builtin_elementwise_min(d, as_us2(R.sphs[k]));
+        bool in = (as_u32(m) == as_u32(d)) & ((uint32_t)(v - R.lov[k]) <= (uint32_t)R.spv[k]);
+        if (ZONES) in &= ((uint32_t)(y - R.r0[k]) < (uint32_t)R.rh[k]) & ((uint32_t)(x - R.c0[k]) < (uint32_t)R.cw[k]);
         excl |= in;
     }
     return !excl;
@@ -129,7 +116,7 @@ struct Sampler {
     const uint8_t* base;  // source pixel (in_x0, in_y0)
     uint32_t pitch, lim;  // lim: last byte offset from base where a dword load fits
     int32_t b0, b1, b2, b3, b4, b5;
-    int32_t in_w, in_h, cn;
+    int32_t in_w, in_h;
 };
 
 __device__ __forceinline__ Sampler make_sampler(const uint8_t* src, const ipp_gather_desc& g) {
@@ -149,19 +136,42 @@ __device__ __forceinline__ Sampler make_sampler(const uint8_t* src, const ipp_ga
     s.b5 = (int32_t)((uint32_t)g.a5 + sy0 * (uint32_t)g.a4 + sx0 * (uint32_t)g.a3);
     s.in_w = g.in_w;
     s.in_h = g.in_h;
-    s.cn = g.src_cn;
     return s;
 }
 
-// Load the source pixel for (xx, yy) in 16.16, or 0 outside (Pillow fill).
-__device__ __forceinline__ uint32_t sample(const Sampler& s, int32_t xx, int32_t yy, bool& valid) {
-    const int xin = xx >> 16, yin = yy >> 16;
-    valid = ((uint32_t)xin < (uint32_t)s.in_w) & ((uint32_t)yin < (uint32_t)s.in_h);
-    if (!valid) return 0u;
-    const uint32_t off = (uint32_t)yin * s.pitch + (uint32_t)(xin * s.cn);
-    if (s.cn == 4) return *reinterpret_cast<const uint32_t*>(s.base + off);
-    const uint32_t d = off > s.lim ? 1u : 0u;  // last pixel of the buffer: shift a dword window
-    return (ld_u32_unaligned(s.base + off - d) >> (8 * d)) | 0xFF000000u;
+// Four horizontally adjacent M pixels: issue the four (branch-free) loads.
+// Invalid lanes read the window origin; `valid` masks them afterwards.
+template <int CN>
+struct Gather4 {
+    uint32_t raw[4];
+    uint32_t sh[4];   // right shift (0 or 8) for a clamped tail load
+    uint32_t valid;   // bit k: pixel k inside the source
+};
+
+template <int CN>
+__device__ __forceinline__ void gather4_issue(const Sampler& S, uint32_t xx, uint32_t yy, Gather4<CN>& G) {
+    G.valid = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int xin = (int32_t)xx >> 16, yin = (int32_t)yy >> 16;
+        const bool ok = ((uint32_t)xin < (uint32_t)S.in_w) & ((uint32_t)yin < (uint32_t)S.in_h);
+        uint32_t off = ok ? (uint32_t)__umul24(yin, S.pitch) + (uint32_t)__umul24(xin, CN) : 0u;
+        if (CN == 3) {
+            const uint32_t offc = min(off, S.lim);
+            G.sh[k] = (off - offc) << 3;
+            off = offc;
+        }
+        G.raw[k] = *reinterpret_cast<const ipp_u32_unaligned*>(S.base + off);
+        G.valid |= (ok ? 1u : 0u) << k;
+        xx += (uint32_t)S.b0;
+        yy += (uint32_t)S.b3;
+    }
+}
+
+template <int CN>
+__device__ __forceinline__ uint32_t gather4_pixel(const Gather4<CN>& G, int k) {
+    const uint32_t p = CN == 3 ? (G.raw[k] >> G.sh[k]) : G.raw[k];
+    return ((G.valid >> k) & 1u) ? (p | 0xFF000000u) : 0u;
 }
 
 // Transpose 4 packed pixels (RGBA each) into 4 channel-planar dwords.
@@ -182,9 +192,10 @@ __device__ int32_t g_dbg_meta[8];
 struct HpassLds {
     uint8_t win[4][HR][WSTRIDE];      // planar window, bytes p ^ 0x80
     uint4 taps[NGL][HX];              // tap planes (P0, P1, P2, -) per group, per output
+    int32_t sdiv[256], hdiv[256];     // OpenCV RGB2HSV_b division tables
 };
 
-template <int NR>
+template <int NR, bool ZONES, int CN>
 __global__ void __launch_bounds__(256)
 k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
              const ipp_pipe_desc* __restrict__ descs, int tiles_x, int tiles_y, ipp_hsv_params hp) {
@@ -199,8 +210,12 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
     const int xo0 = tx * HX, row0 = ty * HR;
     if (xo0 >= h.out_len || row0 >= h.lines) return;  // block-uniform
 
+    for (int i = threadIdx.x; i < 256; i += 256) {
+        L.sdiv[i] = kSdiv[i];
+        L.hdiv[i] = kHdiv180[i];
+    }
     Ranges<NR> R;
-    ranges_init<NR>(R, hp, g.out_w, g.out_h);
+    ranges_init<NR, ZONES>(R, hp, g.out_w, g.out_h);
     const Sampler S = make_sampler(src, g);
     const int ngs = h.ksize;  // tap-group stride of this item (dot4 format)
     const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
@@ -208,6 +223,12 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nrows = min(HR, h.lines - row0);
     const bool taps_in_lds = ngs <= NGL;
+
+    // Phase-1 lane geometry: a wave covers 16 rows × 16 px per step.
+    const int r = lane >> 2;
+    const int y = h.line0 + row0 + r;
+    const uint32_t rowx = (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1;
+    const uint32_t rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
 
     // Outputs of this block: split into sub-chunks whose window fits WSTRIDE.
     const int xo_end = min(xo0 + HX, h.out_len);
@@ -225,39 +246,37 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
                 L.taps[j][o] = (s0 + o < s1) ? planes[(int64_t)(s0 + o) * ngs + j] : make_uint4(0, 0, 0, 0);
             }
         }
+        __syncthreads();  // tables + taps visible
 
-        // Phase 1: M pixels of the window → planar LDS (16 rows × 16 px per wave step).
-        const int r = lane >> 2;
-        const int y = h.line0 + row0 + r;
-        const uint32_t rowx = (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1;
-        const uint32_t rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
-        for (int cg0 = wave * 4; cg0 < ng4; cg0 += 16) {
+        // Phase 1: M pixels of the window → planar LDS; next step's gathers
+        // are in flight while this step's HSV runs.
+        Gather4<CN> cur, nxt;
+        int cg0 = wave * 4;
+        if (cg0 < ng4) {
+            const int x = W0 + 4 * (cg0 + (lane & 3));
+            gather4_issue<CN>(S, rowx + (uint32_t)x * (uint32_t)S.b0, rowy + (uint32_t)x * (uint32_t)S.b3, nxt);
+        }
+        for (; cg0 < ng4; cg0 += 16) {
+            cur = nxt;
             const int cg = cg0 + (lane & 3);
             const int x = W0 + 4 * cg;
-            uint32_t px[4];
-            bool vany = false;
-            uint32_t xx = rowx + (uint32_t)x * (uint32_t)S.b0, yy = rowy + (uint32_t)x * (uint32_t)S.b3;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                bool valid;
-                px[k] = sample(S, (int32_t)xx, (int32_t)yy, valid);
-                vany |= valid;
-                xx += (uint32_t)S.b0;
-                yy += (uint32_t)S.b3;
+            if (cg0 + 16 < ng4) {
+                const int xn = x + 64;
+                gather4_issue<CN>(S, rowx + (uint32_t)xn * (uint32_t)S.b0, rowy + (uint32_t)xn * (uint32_t)S.b3, nxt);
             }
             const bool active = (cg < ng4) && (r < nrows);
-            // waves whose 64 pixels all fall outside the source: every M value
-            // is the (per-item constant) transparent fill — no HSV work.
-            if (__ballot(vany && active) != 0ull) {
+            uint32_t px[4];
+            if (__ballot(cur.valid != 0u && active) != 0ull) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const bool keep = hsv_keep<NR>(R, px[k], x + k, y);
-                    px[k] = keep ? (px[k] | 0xFF000000u) : 0u;  // premultiplied, α ∈ {0, 255}
+                    const uint32_t p = gather4_pixel<CN>(cur, k);
+                    px[k] = hsv_keep<NR, ZONES>(R, L.sdiv, L.hdiv, p, x + k, y) ? (p | 0xFF000000u) : 0u;
                 }
             } else {
                 // all-fill wave: HSV of black is constant, only zones vary
 #pragma unroll
-                for (int k = 0; k < 4; ++k) px[k] = hsv_keep<NR>(R, 0u, x + k, y) ? 0xFF000000u : 0u;
+                for (int k = 0; k < 4; ++k)
+                    px[k] = hsv_keep<NR, ZONES>(R, L.sdiv, L.hdiv, 0u, x + k, y) ? 0xFF000000u : 0u;
             }
             if (active) {
                 uint32_t ch[4];
@@ -268,12 +287,6 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
             }
         }
         __syncthreads();
-#ifdef IPP_DBG_DUMP
-        if (im == 0 && tx == 0 && ty == 0 && s0 == xo0) {
-            for (int i = threadIdx.x; i < 4 * HR * WSTRIDE; i += 256) g_dbg_win[i] = (&L.win[0][0][0])[i];
-            if (threadIdx.x == 0) { g_dbg_meta[0] = W0; g_dbg_meta[1] = ww; g_dbg_meta[2] = ngs; g_dbg_meta[3] = s1; }
-        }
-#endif
 
         // Phase 2: output x' = s0 + lane, rows 4*wave .. 4*wave+3.
         const int xo = s0 + lane;
@@ -285,8 +298,7 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
             for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
                 for (int c = 0; c < 4; ++c) acc[rr][c][0] = acc[rr][c][1] = acc[rr][c][2] = 0;
-            for (int j = 0; j < ngs; ++j) {
-                const uint4 tp = taps_in_lds ? L.taps[j][lane] : planes[(int64_t)xo * ngs + j];
+            auto step = [&](int j, const uint4 tp) {
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     const int row = 4 * wave + rr;
@@ -298,19 +310,19 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
                         acc[rr][c][2] = sdot4(w, tp.z, acc[rr][c][2]);
                     }
                 }
+            };
+            // One tap group per iteration: unrolling j lets the compiler merge
+            // the 4-byte-aligned window reads of j and j+1 into ds_read2_b64,
+            // which gfx950 replays at ~64 cycles when not 8-byte aligned.
+            if (taps_in_lds) {
+#pragma unroll 1
+                for (int j = 0; j < ngs; ++j) step(j, L.taps[j][lane]);
+            } else {
+                const uint4* tpg = planes + (int64_t)xo * ngs;
+#pragma unroll 1
+                for (int j = 0; j < ngs; ++j) step(j, tpg[j]);
             }
             uint32_t outc[4] = {0u, 0u, 0u, 0u};
-#ifdef IPP_DBG_WIN
-            // debug: T <- raw window pixel at column g0(x') (premultiplied M)
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    acc[rr][c][0] = (int32_t)((L.win[c][4 * wave + rr][wo] ^ 0x80u)) << 22, acc[rr][c][1] = 0,
-                    acc[rr][c][2] = 0;
-            const int4 hd0 = make_int4(hd.x, hd.y, 1 << 21, 0);
-#define hd hd0
-#endif
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
@@ -318,9 +330,6 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
                     const int32_t ss = hd.z + acc[rr][c][0] + (acc[rr][c][1] << 8) + (acc[rr][c][2] << 16);
                     outc[c] |= clip8(ss) << (8 * rr);
                 }
-#ifdef IPP_DBG_WIN
-#undef hd
-#endif
             const int grp = (row0 >> 2) + wave;
             uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
             *dst = make_uint4(outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
@@ -424,10 +433,22 @@ k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, u
     }
 }
 
-template <int NR>
+template <int NR, bool ZONES, int CN>
 void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                   const ipp_pipe_desc* descs, int tx, int ty, const ipp_hsv_params& hp) {
-    hipLaunchKernelGGL(k_pipe_hpass<NR>, grid, dim3(256), 0, s, src, tmp, coefs, descs, tx, ty, hp);
+    hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, tx, ty, hp);
+}
+
+template <int NR>
+void launch_hpass_nr(bool zones, int cn, dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp,
+                     const int32_t* coefs, const ipp_pipe_desc* descs, int tx, int ty, const ipp_hsv_params& hp) {
+    if (zones) {
+        if (cn == 4) launch_hpass<NR, true, 4>(grid, s, src, tmp, coefs, descs, tx, ty, hp);
+        else launch_hpass<NR, true, 3>(grid, s, src, tmp, coefs, descs, tx, ty, hp);
+    } else {
+        if (cn == 4) launch_hpass<NR, false, 4>(grid, s, src, tmp, coefs, descs, tx, ty, hp);
+        else launch_hpass<NR, false, 3>(grid, s, src, tmp, coefs, descs, tx, ty, hp);
+    }
 }
 
 }  // namespace
@@ -441,29 +462,42 @@ extern "C" int ipp_dbg_dump(void* win, void* meta) {
 #endif
 
 extern "C" int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
-                              int32_t n_images, int32_t max_out_w, int32_t max_rows, const ipp_hsv_params* hsv,
-                              void* stream) {
+                              int32_t n_images, int32_t max_out_w, int32_t max_rows, int32_t src_cn,
+                              const ipp_hsv_params* hsv, void* stream) {
     if (n_images == 0) return IPP_OK;
     if (!src || !tmp || !coefs || !descs || !hsv || n_images < 0 || max_out_w <= 0 || max_rows <= 0) return IPP_E_ARG;
+    if (src_cn != 3 && src_cn != 4) return IPP_E_ARG;
     const int tx = (max_out_w + HX - 1) / HX, ty = (max_rows + HR - 1) / HR;
     const int64_t blocks = (int64_t)tx * ty * n_images;
     if (blocks >= INT32_MAX) return IPP_E_ARG;
     const dim3 grid((uint32_t)blocks);
     hipStream_t s = (hipStream_t)stream;
+    // Zones are needed unless every range's zone is the whole image (all
+    // margins 0).  The source channel count is uniform over the batch.
+    bool zones = false;
+    for (int k = 0; k < hsv->n_ranges; ++k)
+        for (int m = 0; m < 4; ++m) zones |= hsv->r[k].zone[m] != 0;
+    const int cn = src_cn;
+    // A range that never matches: h - 0xFFFF wraps to h + 1 > span 0.
+    const ipp_hsv_range never = ipp_hsv_range{{0xFFFF, 0, 0}, {0xFFFF, 0, 255}, {0, 0, 0, 0}};
     switch (hsv->n_ranges) {
-        case 0: launch_hpass<0>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        case 1: launch_hpass<1>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        case 2: launch_hpass<2>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        case 3: launch_hpass<3>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        case 4: launch_hpass<4>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        case 5: launch_hpass<5>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        case 6: launch_hpass<6>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        case 7: launch_hpass<7>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        case 8: launch_hpass<8>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        default:
-            if (hsv->n_ranges > IPP_MAX_HSV_RANGES) return IPP_E_ARG;
-            launch_hpass<IPP_MAX_HSV_RANGES>(grid, s, src, tmp, coefs, descs, tx, ty, *hsv);
+        case 1: launch_hpass_nr<1>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 2: launch_hpass_nr<2>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 3: launch_hpass_nr<3>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 4: launch_hpass_nr<4>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 5: case 6: {
+            ipp_hsv_params q = *hsv;  // pad with never-matching ranges (lo > hi in v)
+            for (int k = q.n_ranges; k < 6; ++k) q.r[k] = never;
+            launch_hpass_nr<6>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, q);
             break;
+        }
+        default: {
+            if (hsv->n_ranges > IPP_MAX_HSV_RANGES) return IPP_E_ARG;
+            ipp_hsv_params q = *hsv;
+            for (int k = q.n_ranges; k < IPP_MAX_HSV_RANGES; ++k) q.r[k] = never;
+            launch_hpass_nr<IPP_MAX_HSV_RANGES>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, q);
+            break;
+        }
     }
     IPP_CHECK_LAUNCH();
     return IPP_OK;

@@ -210,7 +210,7 @@ class PipeRunner:
     def hpass(self, src: torch.Tensor) -> None:
         p = self.plan
         N.check(self.lib.ipp_pipe_hpass(src.data_ptr(), self.tmp.data_ptr(), self.coefs.data_ptr(),
-                                        self.descs.data_ptr(), len(p.descs), p.max_out_w, p.max_rows,
+                                        self.descs.data_ptr(), len(p.descs), p.max_out_w, p.max_rows, 3,
                                         N.np_ptr(p.hsv), _stream(self.device)), "ipp_pipe_hpass")
 
     def vblend(self, bgs: torch.Tensor, out: torch.Tensor) -> None:

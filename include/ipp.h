@@ -174,9 +174,10 @@ typedef struct ipp_pipe_desc {
     ipp_paste_desc p;       /* paste: ov = V-pass result (never stored)        */
 } ipp_pipe_desc;
 
+/* src_cn: channels of every source in the batch (3 or 4); hsv: HOST pointer. */
 int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                    const ipp_pipe_desc* descs, int32_t n_images,
-                   int32_t max_out_w, int32_t max_rows,
+                   int32_t max_out_w, int32_t max_rows, int32_t src_cn,
                    const ipp_hsv_params* hsv, void* stream);
 int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
                     const int32_t* coefs, const ipp_pipe_desc* descs, int32_t n_images,
