@@ -91,8 +91,8 @@ SIGNATURES = {
     "ipp_plan_opaque_bbox": (_I, [_I, _I, _P, _I, _I, _P]),
     "ipp_plan_dot4_stride": (_I, [_I]),
     "ipp_plan_dot4_size": (_L, [_I, _I]),
-    "ipp_plan_dot4_from_taps": (_I, [_I, _I, _P, _I, _P]),
-    "ipp_plan_pipe_axes": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _I]),
+    "ipp_plan_dot4_from_taps": (_I, [_I, _I, _P, _I, _I, _P]),
+    "ipp_plan_pipe_axes": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I]),
     "ipp_version": (ctypes.c_char_p, []),
 }
 

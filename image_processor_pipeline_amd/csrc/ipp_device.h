@@ -100,3 +100,49 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nblocks) {
     uint32_t q = nblocks >> 3, r = nblocks & 7u;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
 }
+
+// 16 composite bytes (RGB, 3 per pixel) starting at row byte c0, blended with
+// the RGBA overlay row `ov` (pixels [ox0, ox0 + ov_w)) — Paste.c
+// paste_mask_RGBA: out = DIV255(bg * (255 - a) + ov * a) per channel.  Fully
+// unrolled over register dwords (a dynamically indexed byte array would live
+// in scratch memory).
+template <typename OvFetch>
+__device__ __forceinline__ void blend16(uint32_t w[4], int c0, int nbytes, int ox0, int ov_w, OvFetch fetch) {
+    int px = c0 / 3, ch = c0 - 3 * px;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int ox = px - ox0;
+        if (j < nbytes && (unsigned)ox < (unsigned)ov_w) {
+            const uint32_t o = fetch(ox);
+            const uint32_t a = o >> 24;
+            const uint32_t bgb = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            const uint32_t v = div255(bgb * (255u - a) + ((o >> (8 * ch)) & 0xFFu) * a);
+            w[j >> 2] = (w[j >> 2] & ~(0xFFu << (8 * (j & 3)))) | (v << (8 * (j & 3)));
+        }
+        if (++ch == 3) { ch = 0; ++px; }
+    }
+}
+
+// Load / store up to 16 bytes of a row into 4 register dwords (vector path
+// when 16-B aligned and complete, byte path otherwise).
+__device__ __forceinline__ void load16(const uint8_t* p, int nbytes, bool vec, uint32_t w[4]) {
+    if (vec) {
+        const uint4 v = *reinterpret_cast<const uint4*>(p);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else {
+        w[0] = w[1] = w[2] = w[3] = 0u;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (j < nbytes) w[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
+    }
+}
+
+__device__ __forceinline__ void store16(uint8_t* p, int nbytes, bool vec, const uint32_t w[4]) {
+    if (vec) {
+        *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (j < nbytes) p[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    }
+}

@@ -208,7 +208,7 @@ extern "C" int64_t ipp_plan_dot4_size(int32_t out_size, int32_t ksize) {
 // Convert standard Pillow taps (bounds[2*out] + taps[out*ksize]) into the dot4
 // format; `shift` is subtracted from every xmin (the V pass's ybox_first).
 extern "C" int ipp_plan_dot4_from_taps(int32_t out_size, int32_t ksize, const int32_t* std_taps, int32_t shift,
-                                       int32_t* out) {
+                                       int32_t transposed, int32_t* out) {
     if (out_size <= 0 || ksize <= 0 || !std_taps || !out) return IPP_E_ARG;
     const int ngs = ipp_plan_dot4_stride(ksize);
     const int32_t* bounds = std_taps;
@@ -222,16 +222,24 @@ extern "C" int ipp_plan_dot4_from_taps(int32_t out_size, int32_t ksize, const in
         const int ng = (off + cnt + 3) / 4;
         if (ng > ngs) return IPP_E_RANGE;
         int64_t sum = 0;
-        int32_t* pl = planes + (int64_t)o * ngs * 4;
-        for (int j = 0; j < ngs; ++j) pl[4 * j] = pl[4 * j + 1] = pl[4 * j + 2] = pl[4 * j + 3] = 0;
+        // group j of output o lives at planes[(o*ngs + j)*4] (row-major) or
+        // planes[(j*out_size + o)*4] (transposed: a wave's lanes read 16 B each,
+        // contiguous, for one j).
+        auto grp = [&](int j) -> int32_t* {
+            return planes + 4 * (transposed ? ((int64_t)j * out_size + o) : ((int64_t)o * ngs + j));
+        };
+        for (int j = 0; j < ngs; ++j) {
+            int32_t* pl = grp(j);
+            pl[0] = pl[1] = pl[2] = pl[3] = 0;
+        }
         for (int t = 0; t < cnt; ++t) {
             const int32_t k = kk[(int64_t)o * ksize + t];
             sum += k;
             int8_t b[3];
             balanced_bytes(k, b);
             const int pos = off + t, j = pos >> 2, bb = pos & 3;
-            for (int p = 0; p < 3; ++p)
-                pl[4 * j + p] |= (int32_t)((uint32_t)(uint8_t)b[p] << (8 * bb));
+            int32_t* pl = grp(j);
+            for (int p = 0; p < 3; ++p) pl[p] |= (int32_t)((uint32_t)(uint8_t)b[p] << (8 * bb));
         }
         hdr[4 * o] = g0;
         hdr[4 * o + 1] = ng;
@@ -248,9 +256,10 @@ extern "C" int ipp_plan_dot4_from_taps(int32_t out_size, int32_t ksize, const in
 // (ybox_first, ybox_last) of the unshifted bounds.  offsets[i] = int32 offset
 // of the axis block in `out`, sized by ipp_plan_dot4_size(out, ksize(i)).
 extern "C" int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int32_t* out_sizes,
-                                  const int32_t* identity, const int32_t* shift_first, const int64_t* offsets,
-                                  int32_t* out, int32_t* first_last, int32_t n_threads) {
-    if (n < 0 || (n > 0 && (!in_sizes || !out_sizes || !identity || !shift_first || !offsets || !out || !first_last)))
+                                  const int32_t* identity, const int32_t* shift_first, const int32_t* transposed,
+                                  const int64_t* offsets, int32_t* out, int32_t* first_last, int32_t n_threads) {
+    if (n < 0 || (n > 0 && (!in_sizes || !out_sizes || !identity || !shift_first || !transposed || !offsets || !out ||
+                            !first_last)))
         return IPP_E_ARG;
     int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
     nt = std::max(1, std::min(nt, 64));
@@ -278,7 +287,8 @@ extern "C" int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int3
             const int first = tmp[0], last = tmp[2 * (o - 1)] + tmp[2 * (o - 1) + 1];
             first_last[2 * i] = first;
             first_last[2 * i + 1] = last;
-            const int e = ipp_plan_dot4_from_taps(o, ksize, tmp.data(), shift_first[i] ? first : 0, out + offsets[i]);
+            const int e = ipp_plan_dot4_from_taps(o, ksize, tmp.data(), shift_first[i] ? first : 0, transposed[i],
+                                                  out + offsets[i]);
             if (e) err[t] = e;
         }
     };

@@ -28,7 +28,6 @@ namespace {
 constexpr int HX = 64;            // H-pass outputs per block (one per lane)
 constexpr int HR = 16;            // H-pass rows per block (4 per thread)
 constexpr int WSTRIDE = 400;      // LDS bytes per plane row (≡ 4 dwords mod 32 banks)
-constexpr int NGL = 16;           // tap groups staged in LDS per output
 constexpr int VR = 4;             // composite rows per vblend block
 
 __device__ __forceinline__ int32_t sdot4(uint32_t a, uint32_t b, int32_t c) {
@@ -94,7 +93,10 @@ __device__ __forceinline__ bool hsv_keep(const Ranges<NR>& R, const int32_t* sdi
     const int vmin = min(min(b, g), r);
     const int diff = v - vmin;
     const int sat = (int)(((uint32_t)__umul24(diff, sdiv_t[v]) + 2048u) >> 12);
-    int hh = (v == r) ? (g - b) : ((v == g) ? (b - r + 2 * diff) : (r - g + 4 * diff));
+    // branch-free hue numerator (OpenCV's vr/vg masks): v==r ? g-b : v==g ? b-r+2d : r-g+4d
+    const int h_r = g - b, h_g = b - r + 2 * diff, h_b = r - g + 4 * diff;
+    int hh = (v == g) ? h_g : h_b;
+    hh = (v == r) ? h_r : hh;
     hh = (__mul24(hh, hdiv_t[diff]) + 2048) >> 12;
     hh += hh < 0 ? 180 : 0;
     const us2 hs = as_us2((uint32_t)hh | ((uint32_t)sat << 16));
@@ -155,7 +157,8 @@ __device__ __forceinline__ void gather4_issue(const Sampler& S, uint32_t xx, uin
     for (int k = 0; k < 4; ++k) {
         const int xin = (int32_t)xx >> 16, yin = (int32_t)yy >> 16;
         const bool ok = ((uint32_t)xin < (uint32_t)S.in_w) & ((uint32_t)yin < (uint32_t)S.in_h);
-        uint32_t off = ok ? (uint32_t)__umul24(yin, S.pitch) + (uint32_t)__umul24(xin, CN) : 0u;
+        const uint32_t off_any = (uint32_t)__umul24(yin, S.pitch) + (uint32_t)__umul24(xin, CN);
+        uint32_t off = ok ? off_any : 0u;
         if (CN == 3) {
             const uint32_t offc = min(off, S.lim);
             G.sh[k] = (off - offc) << 3;
@@ -191,7 +194,6 @@ __device__ int32_t g_dbg_meta[8];
 
 struct HpassLds {
     uint8_t win[4][HR][WSTRIDE];      // planar window, bytes p ^ 0x80
-    uint4 taps[NGL][HX];              // tap planes (P0, P1, P2, -) per group, per output
     int32_t sdiv[256], hdiv[256];     // OpenCV RGB2HSV_b division tables
 };
 
@@ -219,10 +221,12 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
     const Sampler S = make_sampler(src, g);
     const int ngs = h.ksize;  // tap-group stride of this item (dot4 format)
     const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
+    // H tap planes are stored transposed, [group j][output x'] (16 B each), so a
+    // wave's 64 lanes read one contiguous KiB per group.
     const uint4* planes = reinterpret_cast<const uint4*>(coefs + h.coef_off + 4 * (int64_t)h.out_len);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform → SGPR
     const int nrows = min(HR, h.lines - row0);
-    const bool taps_in_lds = ngs <= NGL;
 
     // Phase-1 lane geometry: a wave covers 16 rows × 16 px per step.
     const int r = lane >> 2;
@@ -239,14 +243,7 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
         const int ww = hdr[s1 - 1].x + 4 * ngs - W0;  // multiple of 4
         const int ng4 = ww >> 2;
 
-        // Phase 0: stage tap planes (transposed: [group][output]).
-        if (taps_in_lds) {
-            for (int i = threadIdx.x; i < ngs * HX; i += 256) {
-                const int j = i / HX, o = i - j * HX;
-                L.taps[j][o] = (s0 + o < s1) ? planes[(int64_t)(s0 + o) * ngs + j] : make_uint4(0, 0, 0, 0);
-            }
-        }
-        __syncthreads();  // tables + taps visible
+        if (s0 == xo0) __syncthreads();  // HSV tables visible
 
         // Phase 1: M pixels of the window → planar LDS; next step's gathers
         // are in flight while this step's HSV runs.
@@ -314,13 +311,13 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
             // One tap group per iteration: unrolling j lets the compiler merge
             // the 4-byte-aligned window reads of j and j+1 into ds_read2_b64,
             // which gfx950 replays at ~64 cycles when not 8-byte aligned.
-            if (taps_in_lds) {
+            const uint4* tpg = planes + xo;
+            uint4 tp = tpg[0];
 #pragma unroll 1
-                for (int j = 0; j < ngs; ++j) step(j, L.taps[j][lane]);
-            } else {
-                const uint4* tpg = planes + (int64_t)xo * ngs;
-#pragma unroll 1
-                for (int j = 0; j < ngs; ++j) step(j, tpg[j]);
+            for (int j = 0; j < ngs; ++j) {
+                const uint4 cur = tp;
+                if (j + 1 < ngs) tp = tpg[(int64_t)(j + 1) * h.out_len];  // prefetch next group
+                step(j, cur);
             }
             uint32_t outc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -401,34 +398,17 @@ k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, u
         uint8_t* drow = dst + p.dst_off + (int64_t)y * p.dst_pitch;
         const int oy = y - p.y;
         const bool in_rows = (unsigned)oy < (unsigned)p.ov_h;
+        const uint32_t* orw = orow + r * bg_w_max;
         for (int ci = threadIdx.x; ci < chunks; ci += 256) {
             const int c0 = ci << 4;
             const int nbytes = min(16, row_bytes - c0);
             const bool vec = nbytes == 16 &&
                              ((reinterpret_cast<uintptr_t>(brow + c0) | reinterpret_cast<uintptr_t>(drow + c0)) & 15u) == 0;
-            uint8_t vb[16];
-            if (vec) {
-                *reinterpret_cast<uint4*>(vb) = *reinterpret_cast<const uint4*>(brow + c0);
-            } else {
-                for (int j = 0; j < nbytes; ++j) vb[j] = brow[c0 + j];
-            }
-            if (in_rows && c0 + nbytes > 3 * p.x && c0 < 3 * (p.x + p.ov_w)) {
-                int px = c0 / 3, ch = c0 - 3 * px;
-                for (int j = 0; j < nbytes; ++j) {
-                    const int ox = px - p.x;
-                    if ((unsigned)ox < (unsigned)p.ov_w) {
-                        const uint32_t o = orow[r * bg_w_max + ox];
-                        const uint32_t a = o >> 24;
-                        vb[j] = (uint8_t)div255((uint32_t)vb[j] * (255u - a) + ((o >> (8 * ch)) & 0xFFu) * a);
-                    }
-                    if (++ch == 3) { ch = 0; ++px; }
-                }
-            }
-            if (vec) {
-                *reinterpret_cast<uint4*>(drow + c0) = *reinterpret_cast<const uint4*>(vb);
-            } else {
-                for (int j = 0; j < nbytes; ++j) drow[c0 + j] = vb[j];
-            }
+            uint32_t w[4];
+            load16(brow + c0, nbytes, vec, w);
+            if (in_rows && c0 + nbytes > 3 * p.x && c0 < 3 * (p.x + p.ov_w))
+                blend16(w, c0, nbytes, p.x, p.ov_w, [&](int ox) { return orw[ox]; });
+            store16(drow + c0, nbytes, vec, w);
         }
     }
 }

@@ -99,31 +99,14 @@ k_paste_blend(const uint8_t* __restrict__ bg, const uint8_t* __restrict__ ov, ui
     uint8_t* orow = dst + d.dst_off + (int64_t)y * d.dst_pitch;
     const int nbytes = min(16, row_bytes - c0);
     const bool vec = nbytes == 16 && ((reinterpret_cast<uintptr_t>(brow + c0) | reinterpret_cast<uintptr_t>(orow + c0)) & 15u) == 0;
-    uint8_t v[16];
-    if (vec) {
-        *reinterpret_cast<uint4*>(v) = *reinterpret_cast<const uint4*>(brow + c0);
-    } else {
-        for (int j = 0; j < nbytes; ++j) v[j] = brow[c0 + j];
-    }
+    uint32_t w[4];
+    load16(brow + c0, nbytes, vec, w);
     const int oy = y - d.y;
     if ((unsigned)oy < (unsigned)d.ov_h && c0 + nbytes > 3 * d.x && c0 < 3 * (d.x + d.ov_w)) {
         const uint32_t* orow_ov = reinterpret_cast<const uint32_t*>(ov + d.ov_off + (int64_t)oy * d.ov_pitch);
-        int px = c0 / 3, ch = c0 - 3 * px;
-        for (int j = 0; j < nbytes; ++j) {
-            const int ox = px - d.x;
-            if ((unsigned)ox < (unsigned)d.ov_w) {
-                const uint32_t o = orow_ov[ox];
-                const uint32_t a = o >> 24;
-                v[j] = (uint8_t)div255((uint32_t)v[j] * (255u - a) + ((o >> (8 * ch)) & 0xFFu) * a);
-            }
-            if (++ch == 3) { ch = 0; ++px; }
-        }
+        blend16(w, c0, nbytes, d.x, d.ov_w, [&](int ox) { return orow_ov[ox]; });
     }
-    if (vec) {
-        *reinterpret_cast<uint4*>(orow + c0) = *reinterpret_cast<const uint4*>(v);
-    } else {
-        for (int j = 0; j < nbytes; ++j) orow[c0 + j] = v[j];
-    }
+    store16(orow + c0, nbytes, vec, w);
 }
 
 inline int64_t nblocks(int tx, int ty, int n) { return (int64_t)tx * ty * n; }

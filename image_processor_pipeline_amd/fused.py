@@ -150,8 +150,10 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     offs[1:] = np.cumsum(sizes)[:-1]
     coefs = np.zeros(int(sizes.sum()), np.int32)
     first_last = np.zeros(2 * m, np.int32)
+    transp = np.array([j % 2 == 0 for j in range(m)], np.int32)   # H planes [group][output]
     N.check(lib.ipp_plan_pipe_axes(m, N.np_ptr(a_in), N.np_ptr(a_out), N.np_ptr(ident), N.np_ptr(shift),
-                                   N.np_ptr(offs), N.np_ptr(coefs), N.np_ptr(first_last), 0), "ipp_plan_pipe_axes")
+                                   N.np_ptr(transp), N.np_ptr(offs), N.np_ptr(coefs), N.np_ptr(first_last), 0),
+            "ipp_plan_pipe_axes")
 
     # ---- descriptors ----------------------------------------------------
     tmp_off = 0
@@ -191,6 +193,12 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
         t_bytes = pitch * ((rows + 3) // 4)
         algo_h += 3 * hc * wc + t_bytes
         algo_v += t_bytes + 3 * bh * bw + 3 * bh * bw
+    # Processing order: group items by background so that the items pasting
+    # onto one background run back to back (and, through the XCD-aware block
+    # mapping, on one XCD): the 3 MB background then stays in L2/L3 instead of
+    # being re-read from HBM per item.  Outputs keep their item offsets.
+    order = np.argsort(np.array([it.bg_index for it in params]), kind="stable")
+    d = d[order]
     hsv = G.hsv_params(cfg.hsv_ranges, cfg.zones, cfg.use_gimp_scale, bgr=False)
     return PipePlan(d, coefs, hsv, params, cut_dims, ov_dims, max(tmp_off, 256), max_out_w, max_rows, bw, bh,
                     algo_h, algo_v)

@@ -223,14 +223,15 @@ int ipp_plan_lanczos_batch(int32_t n, const int32_t* in_sizes, const int32_t* ou
 int32_t ipp_plan_dot4_stride(int32_t ksize);
 int64_t ipp_plan_dot4_size(int32_t out_size, int32_t ksize);
 int ipp_plan_dot4_from_taps(int32_t out_size, int32_t ksize, const int32_t* std_taps,
-                            int32_t shift, int32_t* out);
+                            int32_t shift, int32_t transposed, int32_t* out);
 /* Plan every axis of a pipe batch in the dot4 format (threaded); identity[i]
  * = no pass on that axis; shift_first[i] = shift bounds to ybox_first;
- * first_last receives (ybox_first, ybox_last) per axis. */
+ * transposed[i] = planes stored [group][output] (H pass) instead of
+ * [output][group] (V pass); first_last receives (ybox_first, ybox_last). */
 int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int32_t* out_sizes,
                        const int32_t* identity, const int32_t* shift_first,
-                       const int64_t* offsets, int32_t* out, int32_t* first_last,
-                       int32_t n_threads);
+                       const int32_t* transposed, const int64_t* offsets, int32_t* out,
+                       int32_t* first_last, int32_t n_threads);
 /* ksize for (in_size, out_size) without computing taps. */
 int32_t ipp_plan_lanczos_ksize(double in0, double in1, int32_t out_size);
 

@@ -39,7 +39,10 @@ def test_dot4_format_is_exact(io, shift):
         std[0:2 * o:2] += shift   # pretend the axis starts `shift` rows later
     ngs = lib.ipp_plan_dot4_stride(k)
     out = np.zeros(lib.ipp_plan_dot4_size(o, k), np.int32)
-    assert lib.ipp_plan_dot4_from_taps(o, k, N.np_ptr(std), shift, N.np_ptr(out)) == 0
+    assert lib.ipp_plan_dot4_from_taps(o, k, N.np_ptr(std), shift, 0, N.np_ptr(out)) == 0
+    outT = np.zeros_like(out)
+    assert lib.ipp_plan_dot4_from_taps(o, k, N.np_ptr(std), shift, 1, N.np_ptr(outT)) == 0
+    assert np.array_equal(outT[4 * o:].reshape(ngs, o, 4).transpose(1, 0, 2), out[4 * o:].reshape(o, ngs, 4))
     hdr = out[:4 * o].reshape(o, 4)
     planes = out[4 * o:].reshape(o, ngs, 4).view(np.uint32)
     rng = np.random.default_rng(0)
