@@ -80,6 +80,17 @@ def load_pmc_traffic(workload: str):
         return None
 
 
+def make_sources(start: int, stop: int, size: int, seed: int, dev) -> torch.Tensor:
+    """Synthetic sources, item i drawn from its own generator (seed, i): the
+    bytes of an item do not depend on how the batch is sharded."""
+    src = torch.empty((stop - start, size, size, 3), dtype=torch.uint8, device=dev)
+    gen = torch.Generator(device=dev)
+    for i in range(start, stop):
+        gen.manual_seed(seed * 1000003 + i)
+        src[i - start].random_(0, 256, generator=gen)
+    return src
+
+
 def cpu_baseline(args):
     from oracle import cpu_pipe
     return cpu_pipe.measure(args.cpu_sample, size=args.size, workload=args.workload)
@@ -91,11 +102,10 @@ def main():
     from image_processor_pipeline_amd import fused, device as D
 
     B, S, K = args.batch, args.size, args.backgrounds
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(args.seed * 1000003 + rank)
-    src = torch.randint(0, 256, (B, S, S, 3), dtype=torch.uint8, device=dev, generator=gen)
+    # weak scaling: B items per GPU; rank r owns global items [r*B, (r+1)*B)
+    start, stop = fused.shard_range(world * B, rank, world)
+    src = make_sources(start, stop, S, args.seed, dev)
 
-    kernels = {}
     t_plan = time.perf_counter()
     if args.workload == "pipe5":
         bgs = torch.empty((K, S, S, 3), dtype=torch.uint8, device=dev)
@@ -106,7 +116,7 @@ def main():
         if world > 1:
             dist.broadcast(bgs, src=0)  # the one exchange step: shared assets over xGMI
         cfg = fused.PipeConfig()
-        plan = fused.plan_pipe((S, S), B, (S, S), K, cfg, seed=args.seed * 7919 + rank)
+        plan = fused.plan_pipe((S, S), B, (S, S), K, cfg, seed=args.seed * 7919, item_range=(start, stop))
         runner = fused.PipeRunner(plan, dev)
         out = torch.empty((B, S, S, 3), dtype=torch.uint8, device=dev)
         algo = {"ipp_pipe_hpass": plan.algo_bytes_hpass, "ipp_pipe_vblend": plan.algo_bytes_vblend}
@@ -114,9 +124,10 @@ def main():
         workload = "5-stage pipe: crop(64px)->rotate(NEAREST,expand,bbox)->flip->HSV mask(4 ref ranges)->LANCZOS+paste"
     else:
         import random
-        rng = random.Random(args.seed + rank)
-        angles = [rng.uniform(1.0, 359.0) for _ in range(B)]
-        flips = [D.SYM_FLIP[rng.sample(["o", "h", "v", "hv"], 1)[0]] for _ in range(B)]
+        rng = random.Random(args.seed)
+        draws = [(rng.uniform(1.0, 359.0), rng.sample(["o", "h", "v", "hv"], 1)[0]) for _ in range(stop)][start:]
+        angles = [a for a, _ in draws]
+        flips = [D.SYM_FLIP[s_] for _, s_ in draws]
         gplan = D.plan_rotate_flip([(S, S, 3)] * B, angles, flips, src_offsets=[i * S * S * 3 for i in range(B)])
         descs = D._to_dev(gplan.descs, dev)
         out = torch.empty(gplan.total_bytes, dtype=torch.uint8, device=dev)

@@ -1,0 +1,36 @@
+"""Device runtime helpers for the file-mode transforms: one ROCm device per
+process (the GPU-owning process of the pipeline), H2D/D2H of HWC uint8
+arrays.  No CPU fallback: without a GPU or libipp.so the transforms raise
+NativeUnavailable."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+_DEVICE = None
+
+
+def device() -> torch.device:
+    global _DEVICE
+    if _DEVICE is None:
+        N.load()
+        if not torch.cuda.is_available():
+            raise N.NativeUnavailable("no ROCm GPU visible: the image_processor_pipeline_amd transforms run on "
+                                      "MI355X only (there is no CPU fallback)")
+        idx = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
+        _DEVICE = torch.device("cuda", idx)
+    return _DEVICE
+
+
+def h2d(a: np.ndarray) -> torch.Tensor:
+    if a.ndim == 2:
+        a = a[..., None]
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device())
+
+
+def d2h(t: torch.Tensor) -> np.ndarray:
+    return t.contiguous().cpu().numpy()

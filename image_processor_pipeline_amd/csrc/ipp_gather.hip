@@ -97,8 +97,10 @@ k_copy_window(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     }
 }
 
-// Alpha bbox: per block min/max over its tile with wave reductions, then four
-// device-scope atomics.  bbox must be pre-set to (INT_MAX, INT_MAX, -1, -1).
+// Bounding box of non-zero pixels (Pillow getbbox(alpha_only=True): the alpha
+// band for LA/RGBA, any band otherwise; also cv2.findNonZero+boundingRect on
+// an alpha plane): per block min/max over its tile with wave reductions, then
+// four device-scope atomics.  bbox is pre-set to (INT_MAX, INT_MAX, -1, -1).
 __global__ void __launch_bounds__(256)
 k_alpha_bbox(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
              int tiles_x, int tiles_y, int32_t* __restrict__ bbox) {
@@ -115,7 +117,16 @@ k_alpha_bbox(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__
         const uint8_t* row = img + d.off + (int64_t)y * d.pitch;
         for (int k = 0; k < PX_PER_THREAD; ++k) {
             const int x = x0 + k;
-            if (x < d.w && row[(int64_t)x * d.cn + (d.cn - 1)] != 0) {
+            bool nz = false;
+            if (x < d.w) {
+                const uint8_t* px = row + (int64_t)x * d.cn;
+                if (d.cn == 2 || d.cn == 4) {
+                    nz = px[d.cn - 1] != 0;  // alpha band (Pillow getbbox alpha_only)
+                } else {
+                    for (int c = 0; c < d.cn; ++c) nz |= px[c] != 0;  // any band non-zero
+                }
+            }
+            if (nz) {
                 xmin = min(xmin, x);
                 xmax = max(xmax, x);
                 ymin = min(ymin, y);

@@ -86,11 +86,30 @@ def draw_params(n: int, src_hw: Tuple[int, int], bg_hw: Tuple[int, int], n_bg: i
     return rng, order
 
 
+def shard_range(n_global: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous block of the global item list owned by `rank`:
+    sizes differ by at most one, lower ranks take the remainder."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    q, rem = divmod(n_global, world)
+    start = rank * q + min(rank, rem)
+    return start, start + q + (1 if rank < rem else 0)
+
+
 def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int, cfg: PipeConfig,
-              seed: int = 0, src_pitch: Optional[int] = None) -> PipePlan:
+              seed: int = 0, src_pitch: Optional[int] = None, item_range: Optional[Tuple[int, int]] = None
+              ) -> PipePlan:
+    """Plan `n` items.  With ``item_range=(start, stop)`` the random stream is
+    drawn for the global items 0..stop-1 in the reference's order and only
+    items [start, stop) are planned (stop - start must equal n): every rank of
+    a sharded run sees exactly the parameters a single process would give
+    those items, so outputs do not depend on the number of GPUs."""
     H, W = src_hw
     bh, bw = bg_hw
-    rng, order = draw_params(n, src_hw, bg_hw, n_bg, cfg, seed)
+    start, stop = item_range if item_range is not None else (0, n)
+    if stop - start != n or start < 0:
+        raise ValueError(f"item_range {item_range} does not hold {n} items")
+    rng, order = draw_params(stop, src_hw, bg_hw, n_bg, cfg, seed)
     t, b, l, r = G.crop_margins(H, W, cfg.margins)
     wc, hc = W - l - r, H - t - b
     d = np.zeros(n, N.PIPE_DESC)
@@ -98,11 +117,10 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     cut_dims, ov_dims = [], []
     # axis list for the batch tap planner: (in, out) pairs, H then V per item
     axes_in, axes_out, identity = [], [], []
-    rot_cache = {}
-    for i in range(n):
+    pool = list(cfg.sym_pool)
+    for gi in range(stop):
         angle = rng.uniform(cfg.angle_min, cfg.angle_max)
-        sym = rng.sample(list(cfg.sym_pool), 1)[0]
-        key = angle
+        sym = rng.sample(pool, 1)[0]
         plan = G.rotation_plan(wc, hc, angle)
         bb = G.rotated_bbox(wc, hc, plan)
         if bb is not None and bb[2] > bb[0] and bb[3] > bb[1]:
@@ -112,10 +130,13 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
         ratio = rng.uniform(cfg.scale_min, cfg.scale_max)
         nw_, nh_ = G.overlay_size(rw, rh, bw, bh, ratio)
         if nw_ <= 0 or nh_ <= 0:
-            raise ValueError(f"item {i}: degenerate overlay size {nw_}x{nh_}")
+            raise ValueError(f"item {gi}: degenerate overlay size {nw_}x{nh_}")
         x = rng.randint(0, bw - nw_)
         y = rng.randint(0, bh - nh_)
-        params.append(ItemParams(angle, sym, order[i % n_bg], ratio, x, y))
+        if gi < start:
+            continue
+        i = gi - start
+        params.append(ItemParams(angle, sym, order[gi % n_bg], ratio, x, y))
         cut_dims.append((rh, rw))
         ov_dims.append((nh_, nw_))
         g = d[i]["g"]

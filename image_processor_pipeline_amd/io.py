@@ -1,0 +1,72 @@
+"""Host-side image codecs with the semantics the reference relies on.
+
+The reference reads/writes files with ``cv2.imread``/``cv2.imwrite`` (BGR
+order; ``IMREAD_COLOR`` drops alpha, ``IMREAD_UNCHANGED`` keeps it) and with
+Pillow (RGB order).  OpenCV is not installed in this image, so the cv2-style
+helpers below are implemented on Pillow's codecs with the same channel
+conventions.  PNG is lossless, so pixel parity holds; JPEG payloads may differ
+in bytes from libjpeg-turbo as used by OpenCV (quality 95 is OpenCV's default).
+Codec work is host CPU work and sits outside the device hot path.
+"""
+from __future__ import annotations
+
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+from PIL import Image
+
+IMREAD_UNCHANGED = -1
+IMREAD_GRAYSCALE = 0
+IMREAD_COLOR = 1
+
+# ultralytics.data.utils.IMG_FORMATS / VID_FORMATS (ultralytics 8.x lists),
+# used by symmetry.py:92 and video.py:31 for extension checks.
+IMG_FORMATS = {"bmp", "dng", "jpeg", "jpg", "mpo", "png", "tif", "tiff", "webp", "pfm", "heic"}
+VID_FORMATS = {"asf", "avi", "gif", "m4v", "mkv", "mov", "mp4", "mpeg", "mpg", "ts", "wmv", "webm"}
+
+
+def imread(path, flags: int = IMREAD_COLOR) -> Optional[np.ndarray]:
+    """cv2.imread: None when the file is missing or not decodable."""
+    try:
+        with Image.open(str(path)) as im:
+            im.load()
+            mode = im.mode
+            if flags == IMREAD_GRAYSCALE:
+                return np.asarray(im.convert("L")).copy()
+            if flags == IMREAD_UNCHANGED:
+                if mode in ("RGBA", "LA", "PA") or (mode == "P" and "transparency" in im.info):
+                    arr = np.asarray(im.convert("RGBA"))
+                    return arr[..., [2, 1, 0, 3]].copy()
+                if mode in ("L", "I;16", "I", "F", "1"):
+                    return np.asarray(im.convert("L")).copy()
+                arr = np.asarray(im.convert("RGB"))
+                return arr[..., ::-1].copy()
+            arr = np.asarray(im.convert("RGB"))
+            return arr[..., ::-1].copy()
+    except (FileNotFoundError, OSError, ValueError):
+        return None
+
+
+def imwrite(path, img: np.ndarray) -> bool:
+    """cv2.imwrite: BGR(A)/gray array → file chosen by extension."""
+    path = str(path)
+    ext = Path(path).suffix.lower()
+    try:
+        if img.ndim == 2:
+            im = Image.fromarray(img, "L")
+        elif img.shape[2] == 4:
+            im = Image.fromarray(np.ascontiguousarray(img[..., [2, 1, 0, 3]]), "RGBA")
+        else:
+            im = Image.fromarray(np.ascontiguousarray(img[..., ::-1]), "RGB")
+        if ext in (".jpg", ".jpeg"):
+            if im.mode == "RGBA":
+                im = im.convert("RGB")
+            im.save(path, quality=95)
+        elif ext == ".png":
+            im.save(path, compress_level=1)
+        else:
+            im.save(path)
+        return True
+    except (OSError, ValueError, KeyError):
+        return False

@@ -1,0 +1,78 @@
+"""crop_from_border / fit_crop — reference transforms/recadrages.py:13-82.
+
+Margins: fraction of the side when < 1, pixels otherwise (`_compute_crop`,
+:7-10); JPG-only input (:23-24); output keeps the input name.  The crop is an
+exact window copy on the GPU (ipp_copy_window); fit_crop uses Pillow's
+getbbox rule via ipp_alpha_bbox."""
+from __future__ import annotations
+
+from pathlib import Path
+from typing import Any, List, Optional, Tuple
+
+import numpy as np
+from PIL import Image
+
+from ._common import device_transform
+from .. import _rt
+from .. import device as D
+from .. import geometry as G
+from .. import io as _io
+
+
+def _compute_crop(value, total_length):
+    return G.compute_crop(value, total_length)
+
+
+@device_transform
+def crop_from_border(
+    file: Path,
+    output_dirs: List[Path],
+    crop_margins: Tuple[float, float, float, float] = (0, 0, 0, 0),
+    **options: Any,
+) -> Optional[Path]:
+    output_dir = Path(output_dirs[0])
+    if file.suffix.lower() not in (".jpg", ".jpeg"):
+        raise ValueError(f"Le Fichier {file.name} n'est pas du type JPG.")
+    crop_top, crop_bottom, crop_left, crop_right = crop_margins
+    image = _io.imread(str(file), _io.IMREAD_UNCHANGED)
+    if image is None:
+        raise FileNotFoundError(f"Impossible de charger l'image {file.name}.")
+    height, width = image.shape[:2]
+    t = _compute_crop(crop_top, height)
+    b = _compute_crop(crop_bottom, height)
+    l = _compute_crop(crop_left, width)
+    r = _compute_crop(crop_right, width)
+    if t + b >= height or l + r >= width:
+        raise ValueError(f"Les marges de rognage sont trop grandes pour l'image {file.name}.")
+    cropped = _rt.d2h(D.copy_window(_rt.h2d(image), (l, t, width - l - r, height - t - b)))
+    if image.ndim == 2:
+        cropped = cropped[..., 0]
+    output_path = output_dir / file.name
+    try:
+        if _io.imwrite(str(output_path), cropped):
+            return output_path
+        print(f"Avertissement [{file.name} - Symétrie]: Échec de sauvegarde (imwrite a retourné False) "
+              f"pour {output_path.name}")
+        return None
+    except Exception as e_save:
+        print(f"Erreur [{file.name} - Symétrie]: Échec de sauvegarde pour {output_path.name}: {e_save}")
+        return None
+
+
+@device_transform
+def fit_crop(image_path: Path, output_dirs: List[Path], **options: Any) -> Optional[List[Path]]:
+    """Crop to Pillow's getbbox() (recadrages.py:63-82)."""
+    output_dir = Path(output_dirs[0])
+    image = Image.open(image_path)
+    arr = np.asarray(image)
+    t = _rt.h2d(arr)
+    bb = D.alpha_bbox([t])[0]
+    if not bb:
+        new_image = image.copy()
+    else:
+        x0, y0, x1, y1 = bb
+        out = _rt.d2h(D.copy_window(t, (x0, y0, x1 - x0, y1 - y0)))
+        new_image = Image.fromarray(out[..., 0] if arr.ndim == 2 else out, image.mode)
+    output_path = output_dir / image_path.name
+    new_image.save(output_path)
+    return output_path

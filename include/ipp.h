@@ -198,8 +198,10 @@ int ipp_ccl_keep_largest(uint8_t* img, const ipp_image_desc* descs, int32_t n_im
                          const int64_t* lab_off, uint32_t* area, int64_t* stats,
                          int32_t* bbox, void* stream);
 
-/* Alpha bbox (Pillow getbbox alpha_only / cv2.findNonZero+boundingRect) of
- * 4-channel images: bbox[i] = (x0, y0, x1, y1) or (-1,-1,-1,-1). */
+/* Bounding box of non-zero pixels, Pillow getbbox() rule (rotations.py:99,
+ * recadrages.py:70): the alpha band for 2/4-channel images, any band for
+ * 1/3-channel ones (also cv2.findNonZero+boundingRect, pixels_isolés.py:77-79).
+ * bbox[i] = (x0, y0, x1, y1) or (-1,-1,-1,-1) when empty. */
 int ipp_alpha_bbox(const uint8_t* img, const ipp_image_desc* descs, int32_t n_images,
                    int32_t max_w, int32_t max_h, int32_t* bbox, void* stream);
 

@@ -1,0 +1,135 @@
+"""Transform plugins on CPU: argument validation that the reference performs
+before any pixel work (same exception types), file naming helpers, and the
+loud failure of the device path when no GPU is present (no CPU fallback)."""
+import random
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from image_processor_pipeline_amd import _native as N
+from image_processor_pipeline_amd import io as ipp_io
+from image_processor_pipeline_amd.labels_math import xywhn2xyxy, xyxy2xywhn
+from image_processor_pipeline_amd.transforms import crop_square, filtres_liste, overlays, recadrages, symmetry
+from image_processor_pipeline_amd.transforms import rotations
+from image_processor_pipeline_amd.transforms import pixels_isolés as pixiso
+from image_processor_pipeline_amd.utils import utils
+
+nogpu = pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
+
+
+def _png(path: Path, arr):
+    Image.fromarray(arr).save(path)
+    return path
+
+
+def test_validate_dirs(tmp_path):
+    with pytest.raises(IndexError):
+        utils._validate_dirs([tmp_path], 2)
+    assert utils._validate_dirs([tmp_path], 1) == tmp_path
+    assert utils._validate_dirs([tmp_path, tmp_path / "l"], 2) == (tmp_path, tmp_path / "l")
+    assert utils.check_path("/abs") == Path("/abs") and utils.check_path("x", "/r") == Path("/r/x")
+
+
+def test_symmetry_validation(tmp_path):
+    p = _png(tmp_path / "a.png", np.zeros((4, 4, 3), np.uint8))
+    with pytest.raises(ValueError):
+        symmetry.generate_symmetries(p, [])
+    with pytest.raises(ValueError):
+        symmetry.generate_symmetries(tmp_path / "a.xyz", [tmp_path])
+    with pytest.raises(ValueError):
+        symmetry.generate_symmetries(p, [tmp_path], pool=["o", "x"])
+    with pytest.raises(ValueError):
+        symmetry.generate_symmetries(p, [tmp_path], choose_random=-1)
+    with pytest.raises(FileNotFoundError):
+        symmetry.generate_symmetries(tmp_path / "missing.png", [tmp_path])
+
+
+def test_crop_from_border_validation(tmp_path):
+    with pytest.raises(ValueError):
+        recadrages.crop_from_border(tmp_path / "a.png", [tmp_path])
+    with pytest.raises(FileNotFoundError):
+        recadrages.crop_from_border(tmp_path / "a.jpg", [tmp_path])
+    p = tmp_path / "b.jpg"
+    Image.fromarray(np.zeros((10, 10, 3), np.uint8)).save(p)
+    with pytest.raises(ValueError):
+        recadrages.crop_from_border(p, [tmp_path], crop_margins=(5, 5, 0, 0))
+    assert recadrages._compute_crop(0.25, 100) == 25 and recadrages._compute_crop(7, 100) == 7
+
+
+def test_filtres_liste_validation(tmp_path):
+    p = _png(tmp_path / "a.png", np.zeros((4, 4, 3), np.uint8))
+    with pytest.raises(ValueError):
+        filtres_liste.process_images_with_color_masks(p, [tmp_path], [])
+    with pytest.raises(ValueError):
+        filtres_liste.process_images_with_color_masks(p, [tmp_path], [(0, 0, 0, 10, 255, 255)], zones=[None, None])
+    with pytest.raises(IndexError):
+        filtres_liste.process_images_with_color_masks(p, [], [(0, 0, 0, 10, 255, 255)])
+
+
+def test_pixels_isoles_validation(tmp_path):
+    with pytest.raises(ValueError):
+        pixiso.keep_largest_component(tmp_path / "a.jpg", [tmp_path])
+    with pytest.raises(FileNotFoundError):
+        pixiso.keep_largest_component(tmp_path / "missing.png", [tmp_path])
+    p = _png(tmp_path / "rgb.png", np.zeros((4, 4, 3), np.uint8))
+    with pytest.raises(AttributeError):
+        pixiso.keep_largest_component(p, [tmp_path])
+    g = _png(tmp_path / "g.png", np.zeros((4, 4), np.uint8))
+    with pytest.raises(IndexError):
+        pixiso.keep_largest_component(g, [tmp_path])
+
+
+def test_overlays_and_rotations_error_style(tmp_path, capsys):
+    assert overlays.paste_overlay_onto_background(tmp_path / "no.png", tmp_path / "no2.png",
+                                                  [tmp_path, tmp_path]) is None
+    assert "Fichier non trouvé" in capsys.readouterr().out
+    assert rotations.process_rotations(tmp_path / "no.png", [tmp_path]) is None
+    assert rotations.process_rotations(tmp_path / "no.png", []) is None
+    assert overlays._convert_to_yolo_bbox(100, 50, (10, 10, 30, 20)) == (0.2, 0.3, 0.2, 0.2)
+    with pytest.raises(ValueError):
+        overlays._convert_to_yolo_bbox(0, 50, (0, 0, 1, 1))
+
+
+def test_crop_square_validation(tmp_path):
+    img = _png(tmp_path / "a.png", np.zeros((8, 8, 3), np.uint8))
+    lbl = tmp_path / "a.txt"
+    lbl.write_text("0 0.5 0.5 0.25 0.25\n")
+    with pytest.raises(IndexError):
+        crop_square.process_square_crop_around_bbox(img, lbl, [tmp_path])
+    with pytest.raises(FileNotFoundError):
+        crop_square.process_square_crop_around_bbox(tmp_path / "x.png", lbl, [tmp_path, tmp_path])
+    with pytest.raises(FileNotFoundError):
+        crop_square.process_square_crop_around_bbox(img, tmp_path / "x.txt", [tmp_path, tmp_path])
+
+
+def test_labels_math_roundtrip():
+    rng = np.random.default_rng(0)
+    b = rng.uniform(0.1, 0.4, (20, 4))
+    b[:, :2] += 0.3
+    xyxy = xywhn2xyxy(b, 640, 480)
+    assert np.allclose(xyxy2xywhn(xyxy, 640, 480), b)
+    assert np.allclose(xyxy2xywhn(np.array([[10, 10, 30, 20]]), 100, 50), [[0.2, 0.3, 0.2, 0.2]])
+
+
+def test_io_cv2_semantics(tmp_path):
+    rgba = np.random.default_rng(1).integers(0, 256, (5, 6, 4), np.uint8)
+    p = _png(tmp_path / "x.png", rgba)
+    assert np.array_equal(ipp_io.imread(p), rgba[..., 2::-1])                 # IMREAD_COLOR drops α, BGR
+    assert np.array_equal(ipp_io.imread(p, ipp_io.IMREAD_UNCHANGED), rgba[..., [2, 1, 0, 3]])
+    assert ipp_io.imread(tmp_path / "none.png") is None
+    assert ipp_io.imwrite(tmp_path / "y.png", rgba) and np.array_equal(ipp_io.imread(tmp_path / "y.png", -1), rgba)
+
+
+@nogpu
+def test_device_path_fails_loudly_without_gpu(tmp_path):
+    p = _png(tmp_path / "a.png", np.zeros((4, 4, 3), np.uint8))
+    random.seed(0)
+    with pytest.raises(N.NativeUnavailable):
+        symmetry.generate_symmetries(p, [tmp_path])
+    q = tmp_path / "b.jpg"
+    Image.fromarray(np.zeros((10, 10, 3), np.uint8)).save(q)
+    with pytest.raises(N.NativeUnavailable):
+        recadrages.crop_from_border(q, [tmp_path], crop_margins=(1, 1, 1, 1))
