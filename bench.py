@@ -66,16 +66,18 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
-def load_pmc_traffic(workload: str):
+def load_pmc_traffic(workload: str, kernel: str, batch: int):
     """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
     PMC summary (profiles/pmc_traffic.json, produced by tools/pmc_traffic.py
-    from separate --pmc passes, gfx950 FETCH_SIZE ×2 correction applied)."""
+    from separate FETCH_SIZE / WRITE_SIZE passes of this bench at the default
+    batch, gfx950 FETCH_SIZE ×2 correction applied).  None when absent or
+    measured at another batch."""
     f = ROOT / "profiles" / "pmc_traffic.json"
-    if not f.exists():
-        return None
     try:
-        d = json.loads(f.read_text())
-        return d.get(workload)
+        d = json.loads(f.read_text())[workload]
+        if d.get("_batch") not in (None, batch):
+            return None
+        return int(d[kernel]["hbm_bytes"])
     except Exception:
         return None
 
@@ -190,7 +192,7 @@ def main():
                    "parallelism": f"dp{world} (item sharding, RCCL broadcast of backgrounds)"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": load_pmc_traffic(args.workload),
+                     "traffic": load_pmc_traffic(args.workload, dominant, B),
                      "algo_bytes_per_launch": int(algo[dominant]),
                      "avg_launch_ms": round(per_kernel_ms[dominant], 4)},
         "step_hbm_gbps_algorithmic": round(step_algo / (ms_step * 1e-3) / 1e9, 1),

@@ -1,0 +1,61 @@
+"""Per-launch HBM traffic from rocprofv3 PMC passes → profiles/pmc_traffic.json.
+
+Input: a tools/profile.sh output directory holding the separate `fetch`
+(--pmc FETCH_SIZE) and `write` (--pmc WRITE_SIZE) passes of one bench
+command.  Units and corrections (MI355X_MICROARCH.md §HBM): rocprofv3
+reports both counters in KiB; on gfx950 FETCH_SIZE tallies half the bytes
+of wide coalesced streaming reads, so it is doubled.  Infinity-cache hits
+are counted by these memory-side counters, so the figure is an upper
+bound on true HBM bytes.
+
+  python tools/pmc_traffic.py <profile_dir> <workload> <batch> [profiles/pmc_traffic.json]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNELS = {  # C-ABI entry point → device kernel symbol
+    "ipp_pipe_hpass": "k_pipe_hpass",
+    "ipp_pipe_vblend": "k_pipe_vblend",
+    "ipp_rotate_flip_nearest": "k_rotate_flip_nearest",
+}
+
+
+def per_dispatch(d: str, counter: str):
+    vals = defaultdict(lambda: defaultdict(float))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            vals[r["Kernel_Name"]][r.get("Dispatch_Id", r.get("Correlation_Id", ""))] += float(r["Counter_Value"])
+    return vals
+
+
+def main():
+    prof, workload, batch = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    out = sys.argv[4] if len(sys.argv) > 4 else os.path.join("profiles", "pmc_traffic.json")
+    fetch = per_dispatch(os.path.join(prof, "fetch"), "FETCH_SIZE")
+    write = per_dispatch(os.path.join(prof, "write"), "WRITE_SIZE")
+    res = {"_batch": batch}
+    for api, sym in KERNELS.items():
+        fk = [k for k in fetch if sym in k]
+        wk = [k for k in write if sym in k]
+        if not fk or not wk:
+            continue
+        fv = [v for k in fk for v in fetch[k].values()]
+        wv = [v for k in wk for v in write[k].values()]
+        f_bytes = 2 * 1024 * sum(fv) / len(fv)
+        w_bytes = 1024 * sum(wv) / len(wv)
+        res[api] = {"hbm_bytes": int(f_bytes + w_bytes), "fetch_bytes_x2": int(f_bytes), "write_bytes": int(w_bytes),
+                    "dispatches": len(fv)}
+    data = json.load(open(out)) if os.path.exists(out) else {}
+    data[workload] = res
+    json.dump(data, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
