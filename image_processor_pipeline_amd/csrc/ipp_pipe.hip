@@ -48,17 +48,31 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
-// Per-block uniform HSV range state (SGPRs).  h and s are tested together as
-// packed 16-bit lanes: d = (h,s) - lo (wrapping), in range ⟺ min(d, span) == d.
-typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+// 24-bit multiply-add, exact for the HSV table products (|a| < 2^11,
+// |b| < 2^21, result < 2^31).  Written as VOP3 so the compiler cannot widen it
+// to the quarter-rate v_mad_u64_u32 it otherwise picks for this pattern.
+__device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ int32_t mad_i24(int32_t a, int32_t b, int32_t c) {
+    int32_t d;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
 
-__device__ __forceinline__ uint32_t as_u32(us2 v) { return __builtin_bit_cast(uint32_t, v); }
-__device__ __forceinline__ us2 as_us2(uint32_t v) { return __builtin_bit_cast(us2, v); }
+// Per-block uniform HSV range state (SGPRs).  (h, s, v) are packed as 10-bit
+// fields X0 = h | s << 10 | v << 20; with guard bits G at 9/19/29,
+//   (X0|G) - lo  keeps field guard f  ⟺  x_f >= lo_f,
+//   (hi|G) - X0  keeps field guard f  ⟺  x_f <= hi_f,
+// so a range holds iff every guard survives both subtractions (no borrow can
+// cross a field: x_f, lo_f, hi_f <= 255 < 512).
+constexpr uint32_t kGuard = (1u << 9) | (1u << 19) | (1u << 29);
 
 template <int NR>
 struct Ranges {
-    uint32_t lohs[NR], sphs[NR];   // (lo_h | lo_s << 16), (span_h | span_s << 16)
-    int32_t lov[NR], spv[NR];
+    uint32_t lo[NR], hig[NR];
     int32_t r0[NR], rh[NR], c0[NR], cw[NR];
 };
 
@@ -67,10 +81,8 @@ __device__ __forceinline__ void ranges_init(Ranges<NR>& R, const ipp_hsv_params&
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
         const ipp_hsv_range& q = hp.r[k];
-        R.lohs[k] = (uint32_t)q.lo[0] | ((uint32_t)q.lo[1] << 16);
-        R.sphs[k] = (uint32_t)(q.hi[0] - q.lo[0]) | ((uint32_t)(q.hi[1] - q.lo[1]) << 16);
-        R.lov[k] = q.lo[2];
-        R.spv[k] = q.hi[2] - q.lo[2];
+        R.lo[k] = (uint32_t)q.lo[0] | ((uint32_t)q.lo[1] << 10) | ((uint32_t)q.lo[2] << 20);
+        R.hig[k] = ((uint32_t)q.hi[0] | ((uint32_t)q.hi[1] << 10) | ((uint32_t)q.hi[2] << 20)) | kGuard;
         if (ZONES) {
             int a, b, cc, dd;
             slice_indices(q.zone[0], h - q.zone[1], h, a, b);
@@ -86,30 +98,36 @@ __device__ __forceinline__ void ranges_init(Ranges<NR>& R, const ipp_hsv_params&
 // OpenCV RGB2HSV_b (hsv_shift 12; sdiv/hdiv tables in LDS) + the union of
 // inRange boxes (and zones) → keep?
 template <int NR, bool ZONES>
-__device__ __forceinline__ bool hsv_keep(const Ranges<NR>& R, const int32_t* sdiv_t, const int32_t* hdiv_t,
+__device__ __forceinline__ uint32_t hsv_keep(const Ranges<NR>& R, const int32_t* sdiv_t, const int32_t* hdiv_t,
                                          uint32_t px, int x, int y) {
     const int r = px & 0xFF, g = (px >> 8) & 0xFF, b = (px >> 16) & 0xFF;  // Pillow order
     const int v = max(max(b, g), r);
     const int vmin = min(min(b, g), r);
     const int diff = v - vmin;
-    const int sat = (int)(((uint32_t)__umul24(diff, sdiv_t[v]) + 2048u) >> 12);
+    const uint32_t sat = mad_u24((uint32_t)diff, (uint32_t)sdiv_t[v], 2048u) >> 12;
     // branch-free hue numerator (OpenCV's vr/vg masks): v==r ? g-b : v==g ? b-r+2d : r-g+4d
     const int h_r = g - b, h_g = b - r + 2 * diff, h_b = r - g + 4 * diff;
     int hh = (v == g) ? h_g : h_b;
     hh = (v == r) ? h_r : hh;
-    hh = (__mul24(hh, hdiv_t[diff]) + 2048) >> 12;
-    hh += hh < 0 ? 180 : 0;
-    const us2 hs = as_us2((uint32_t)hh | ((uint32_t)sat << 16));
-    bool excl = false;
+    // h < 0 → h + 180, as min over unsigned (a negative h wraps above h + 180)
+    const uint32_t hu = (uint32_t)(mad_i24(hh, hdiv_t[diff], 2048) >> 12);
+    const uint32_t hp = min(hu, hu + 180u);
+    const uint32_t x0 = hp | (sat << 10) | ((uint32_t)v << 20);
+    const uint32_t xg = x0 | kGuard;
+    uint32_t nmin = 1u;  // 0 ⟺ some range contains the pixel, else 1
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
-        const us2 d = hs - as_us2(R.lohs[k]);
-        const us2 m = __builtin_elementwise_min(d, as_us2(R.sphs[k]));
-        bool in = (as_u32(m) == as_u32(d)) & ((uint32_t)(v - R.lov[k]) <= (uint32_t)R.spv[k]);
-        if (ZONES) in &= ((uint32_t)(y - R.r0[k]) < (uint32_t)R.rh[k]) & ((uint32_t)(x - R.c0[k]) < (uint32_t)R.cw[k]);
-        excl |= in;
+        uint32_t n = ~((xg - R.lo[k]) & (R.hig[k] - x0)) & kGuard;
+        if (ZONES) n |= (((uint32_t)(y - R.r0[k]) < (uint32_t)R.rh[k]) & ((uint32_t)(x - R.c0[k]) < (uint32_t)R.cw[k])) ? 0u : 1u;
+        nmin = min(nmin, n);
     }
-    return !excl;
+    return nmin;
+}
+
+// Opaque M pixel (alpha 255) when kept, else transparent black: 0 - keep is
+// the all-ones mask.
+__device__ __forceinline__ uint32_t keep_pixel(uint32_t p, uint32_t keep) {
+    return (p | 0xFF000000u) & (0u - keep);
 }
 
 // Source sampling for M pixel (x, y): flip + bbox offset folded into the 16.16
@@ -267,13 +285,13 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint32_t p = gather4_pixel<CN>(cur, k);
-                    px[k] = hsv_keep<NR, ZONES>(R, L.sdiv, L.hdiv, p, x + k, y) ? (p | 0xFF000000u) : 0u;
+                    px[k] = keep_pixel(p, hsv_keep<NR, ZONES>(R, L.sdiv, L.hdiv, p, x + k, y));
                 }
             } else {
                 // all-fill wave: HSV of black is constant, only zones vary
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    px[k] = hsv_keep<NR, ZONES>(R, L.sdiv, L.hdiv, 0u, x + k, y) ? 0xFF000000u : 0u;
+                    px[k] = keep_pixel(0u, hsv_keep<NR, ZONES>(R, L.sdiv, L.hdiv, 0u, x + k, y));
             }
             if (active) {
                 uint32_t ch[4];
@@ -339,6 +357,7 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
 
 // V pass over T (dot4) → unpremultiply → blend onto the background, fused with
 // the background copy.  Block = VR composite rows.
+template <int STORE>
 __global__ void __launch_bounds__(256)
 k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
               const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int tiles_y, int bg_w_max) {
@@ -408,7 +427,7 @@ k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, u
             load16(brow + c0, nbytes, vec, w);
             if (in_rows && c0 + nbytes > 3 * p.x && c0 < 3 * (p.x + p.ov_w))
                 blend16(w, c0, nbytes, p.x, p.ov_w, [&](int ox) { return orw[ox]; });
-            store16(drow + c0, nbytes, vec, w);
+            store16<STORE>(drow + c0, nbytes, vec, w);
         }
     }
 }
@@ -458,8 +477,8 @@ extern "C" int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* c
     for (int k = 0; k < hsv->n_ranges; ++k)
         for (int m = 0; m < 4; ++m) zones |= hsv->r[k].zone[m] != 0;
     const int cn = src_cn;
-    // A range that never matches: h - 0xFFFF wraps to h + 1 > span 0.
-    const ipp_hsv_range never = ipp_hsv_range{{0xFFFF, 0, 0}, {0xFFFF, 0, 255}, {0, 0, 0, 0}};
+    // A range that never matches: lo_v = 1 > hi_v = 0 (cv::inRange's empty range).
+    const ipp_hsv_range never = ipp_hsv_range{{0, 0, 1}, {180, 255, 0}, {0, 0, 0, 0}};
     switch (hsv->n_ranges) {
         case 1: launch_hpass_nr<1>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
         case 2: launch_hpass_nr<2>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
@@ -493,8 +512,20 @@ extern "C" int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* d
     const int ty = (bg_h + VR - 1) / VR;
     const int64_t blocks = (int64_t)ty * n_images;
     if (blocks >= INT32_MAX) return IPP_E_ARG;
-    hipLaunchKernelGGL(k_pipe_vblend, dim3((uint32_t)blocks), dim3(256), shmem, (hipStream_t)stream, tmp, bg, dst,
-                       coefs, descs, ty, bg_w);
+    // Composite store policy (IPP_VB_STORE = 0 plain, 1 sc1, 2 nt; default sc1:
+    // the write-once output then does not evict the shared backgrounds).
+    static const int policy = [] {
+        const char* e = getenv("IPP_VB_STORE");
+        return e ? atoi(e) : 1;
+    }();
+    const dim3 grid((uint32_t)blocks);
+    hipStream_t s = (hipStream_t)stream;
+    if (policy == 0)
+        hipLaunchKernelGGL(k_pipe_vblend<0>, grid, dim3(256), shmem, s, tmp, bg, dst, coefs, descs, ty, bg_w);
+    else if (policy == 2)
+        hipLaunchKernelGGL(k_pipe_vblend<2>, grid, dim3(256), shmem, s, tmp, bg, dst, coefs, descs, ty, bg_w);
+    else
+        hipLaunchKernelGGL(k_pipe_vblend<1>, grid, dim3(256), shmem, s, tmp, bg, dst, coefs, descs, ty, bg_w);
     IPP_CHECK_LAUNCH();
     return IPP_OK;
 }
