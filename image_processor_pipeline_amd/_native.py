@@ -54,6 +54,9 @@ HSV_PARAMS = np.dtype([("n_ranges", _I4), ("bgr", _I4), ("r", HSV_RANGE, (IPP_MA
 
 IMAGE_DESC = np.dtype([("off", _I8), ("w", _I4), ("h", _I4), ("pitch", _I4), ("cn", _I4)], align=True)
 
+CCL_WORK = np.dtype([("lab_off", _I8), ("p_off", _I8), ("a_off", _I8), ("ent_off", _I8), ("ent_cap", _I8)],
+                    align=True)
+
 RESAMPLE_DESC = np.dtype([
     ("src_off", _I8), ("dst_off", _I8), ("src_pitch", _I4), ("dst_pitch", _I4),
     ("in_len", _I4), ("out_len", _I4), ("lines", _I4), ("line0", _I4), ("ksize", _I4), ("pad_", _I4),
@@ -77,13 +80,16 @@ _D = ctypes.c_double
 SIGNATURES = {
     "ipp_rotate_flip_nearest": (_I, [_P, _P, _P, _I, _I, _I, _P]),
     "ipp_copy_window": (_I, [_P, _P, _P, _I, _I, _I, _P]),
+    "ipp_crop_to_bbox": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ipp_hsv_mask": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "ipp_lanczos_h": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ipp_lanczos_v": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ipp_paste_blend": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     "ipp_pipe_hpass": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "ipp_pipe_vblend": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
-    "ipp_ccl_keep_largest": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "ipp_ccl_keep_largest": (_I, [_P, _P, _I, _I, _I, _P, _P, _L, _P, _P, _P, _P]),
+    "ipp_ccl_scratch_layout": (_L, [_I, _I, _P]),
+    "ipp_video_keep_largest": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _L, _P, _P, _P, _P, _P, _P]),
     "ipp_alpha_bbox": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "ipp_plan_lanczos": (_L, [_I, _D, _D, _I, _P, _L]),
     "ipp_plan_lanczos_ksize": (_I, [_D, _D, _I]),

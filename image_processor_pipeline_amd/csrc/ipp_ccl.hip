@@ -1,4 +1,5 @@
-// ipp_ccl.hip — K10..K13: pixels_isolés.keep_largest_component.
+// ipp_ccl.hip — K10..K13: pixels_isolés.keep_largest_component, and the fused
+// config-5 chain (filtres_liste HSV mask → keep largest → crop-fit).
 //
 // Reference: pixels_isolés.py:32 threshold(α, 1, 255, BINARY) → fg = α > 1;
 // :35 connectedComponentsWithStats(fg, connectivity=8); :38-44 largest area,
@@ -6,55 +7,80 @@
 // (when there is no foreground at all, label 0 — the background — is "kept"
 // and α is left unchanged); :74-81 crop-fit to the bbox of α ≠ 0.
 //
-// Labels live in BLOCK-RASTER index space: pixel (x, y) ↦
-//   L = ((y >> 1) * wb + (x >> 1)) * 4 + (y & 1) * 2 + (x & 1),  wb = ⌈w/2⌉.
-// Union-find always links the larger index under the smaller, so a
-// component's root is its minimum L, and root >> 2 is the first 2×2 scan block
-// (in raster order of blocks) that touches it — the order in which OpenCV's
-// block-based 8-connectivity labelling (Spaghetti/BBDT) numbers components.
-// The tie rule is therefore "smallest root", restated (UNPINNED: OpenCV is
-// absent here).  All four pixels of a 2×2 block are mutually 8-adjacent, so
-// no two components share a block.
+// Component identity.  Pixel (x, y) has the BLOCK-RASTER index
+//   L = ((y >> 1) * wb + (x >> 1)) * 4 + (y & 1) * 2 + (x & 1),  wb = ⌈w/2⌉,
+// and every union links the larger index under the smaller, so a component's
+// root is its minimum L: root >> 2 is the first 2×2 scan block (blocks in
+// raster order) that touches it — the order in which OpenCV's block-based
+// 8-connectivity labelling (Spaghetti/BBDT) numbers components.  The tie rule
+// is therefore "smallest root" (restated; UNPINNED: OpenCV is absent here).
 //
-// Union: lock-free atomicMin linking (Playne–Hawick style); parents only
-// decrease, so stale reads cost extra iterations, never a wrong answer.
-#include "ipp_device.h"
+// Algorithm (tile-local labelling, then border merging):
+//   K1 k_ccl_tile     one 64×32 tile per block: fg bits (α > 1, or the fused
+//                     HSV mask) → LDS union-find → per-pixel local root
+//                     (uint16, raster) + one entry per local component
+//                     {global root index, area}; P[root] = root, A[root] = 0.
+//   K2 k_ccl_border   unites the local roots of 8-adjacent fg pixel pairs that
+//                     straddle a tile border (global atomicMin union-find on
+//                     P, touched only at local roots).
+//   K3 k_ccl_resolve  per entry: R = find(P, L); A[R] += area; P[L] = R.
+//   K4 k_ccl_best     per entry that is a global root: atomicMax of
+//                     (area << 32 | ~root) per image.
+//   K5 k_ccl_bbox     bbox of the best component's pixels.
+//   K6 k_ccl_emit     in place: α := 0 outside the best component (plugin
+//                     path), or crop-fit into an output slot writing BGRA with
+//                     α = 255 inside the component (fused chain).
+// Every pixel is read once in K1 and once in K5/K6; P/A/entries are touched
+// per component, not per pixel.
+#include <algorithm>
+
+#include "ipp_hsv.h"
 
 namespace {
 
-constexpr int CHUNK = 1024;  // index-space entries per block (4 per thread)
+constexpr int TW = 64, TH = 32, TPX = TW * TH;  // tile (2048 pixels)
+constexpr uint16_t NOFG = 0xFFFF;
 
-struct Geo {
-    int w, h, wb, hb;
-    int64_t size;  // 4 * wb * hb
+struct Frame {
+    int w, h, wb, tiles_x, tiles_y;
 };
 
-__device__ __forceinline__ Geo geo_of(const ipp_image_desc& d) {
-    Geo g;
-    g.w = d.w;
-    g.h = d.h;
-    g.wb = (d.w + 1) >> 1;
-    g.hb = (d.h + 1) >> 1;
-    g.size = 4ll * g.wb * g.hb;
-    return g;
+__device__ __forceinline__ Frame frame_of(const ipp_image_desc& d) {
+    Frame f;
+    f.w = d.w;
+    f.h = d.h;
+    f.wb = (d.w + 1) >> 1;
+    f.tiles_x = (d.w + TW - 1) / TW;
+    f.tiles_y = (d.h + TH - 1) / TH;
+    return f;
 }
 
-__device__ __forceinline__ void decode(const Geo& g, int64_t L, int& x, int& y) {
-    const int64_t blk = L >> 2;
-    const int by = (int)(blk / g.wb), bx = (int)(blk - (int64_t)by * g.wb);
-    x = 2 * bx + (int)(L & 1);
-    y = 2 * by + (int)((L >> 1) & 1);
+__device__ __forceinline__ int32_t gidx(const Frame& f, int x, int y) {
+    return (((y >> 1) * f.wb + (x >> 1)) << 2) + ((y & 1) << 1) + (x & 1);
 }
 
-__device__ __forceinline__ int32_t encode(const Geo& g, int x, int y) {
-    return (int32_t)((((int64_t)(y >> 1) * g.wb + (x >> 1)) << 2) + ((y & 1) << 1) + (x & 1));
+// Local (in-tile) index with the same ordering as gidx among the tile's pixels.
+__device__ __forceinline__ int lidx(int lx, int ly) {
+    return (((ly >> 1) * (TW / 2) + (lx >> 1)) << 2) + ((ly & 1) << 1) + (lx & 1);
+}
+__device__ __forceinline__ void lpos(int li, int& lx, int& ly) {
+    const int blk = li >> 2;
+    ly = ((blk / (TW / 2)) << 1) + ((li >> 1) & 1);
+    lx = ((blk % (TW / 2)) << 1) + (li & 1);
+}
+
+// Global index of the local root `lr` of tile (tx, ty).
+__device__ __forceinline__ int32_t root_gidx(const Frame& f, int tx, int ty, int lr) {
+    int lx, ly;
+    lpos(lr, lx, ly);
+    return gidx(f, tx * TW + lx, ty * TH + ly);
 }
 
 __device__ __forceinline__ int32_t ld(const int32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ int32_t find_root(const int32_t* P, int32_t x) {
+__device__ __forceinline__ int32_t gfind(const int32_t* P, int32_t x) {
     int32_t p = ld(P + x);
     while (p != x) {
         x = p;
@@ -63,165 +89,291 @@ __device__ __forceinline__ int32_t find_root(const int32_t* P, int32_t x) {
     return x;
 }
 
-__device__ __forceinline__ void unite(int32_t* P, int32_t a, int32_t b) {
-    bool done;
-    do {
-        a = find_root(P, a);
-        b = find_root(P, b);
-        if (a < b) {
-            const int32_t old = atomicMin(P + b, a);
-            done = (old == b);
-            b = old;
-        } else if (b < a) {
-            const int32_t old = atomicMin(P + a, b);
-            done = (old == a);
-            a = old;
-        } else {
-            done = true;
+__device__ __forceinline__ void gunite(int32_t* P, int32_t a, int32_t b) {
+    for (;;) {
+        a = gfind(P, a);
+        b = gfind(P, b);
+        if (a == b) return;
+        if (a > b) {
+            const int32_t t = a;
+            a = b;
+            b = t;
         }
-    } while (!done);
+        const int32_t old = atomicMin(P + b, a);
+        if (old == b) return;
+        b = old;
+    }
 }
 
-struct Block {
-    int im;
-    int64_t base;
+__device__ __forceinline__ int lld(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ int lfind(const int* lab, int x) {
+    int p = lld(lab + x);
+    while (p != x) {
+        x = p;
+        p = lld(lab + x);
+    }
+    return x;
+}
+
+__device__ __forceinline__ void lunite(int* lab, int a, int b) {
+    for (;;) {
+        a = lfind(lab, a);
+        b = lfind(lab, b);
+        if (a == b) return;
+        if (a > b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        const int old = atomicMin(lab + b, a);
+        if (old == b) return;
+        b = old;
+    }
+}
+
+// Scratch layout per image (offsets in the ipp_ccl_work descriptor).
+struct Work {
+    uint16_t* lab16;   // w*h local roots (raster); NOFG for background
+    int32_t* P;        // 4*wb*hb parent array (touched at local roots only)
+    uint32_t* A;       // 4*wb*hb areas (touched at roots only)
+    int32_t* entL;     // per local component: global root index
+    uint32_t* entA;    // ... and its in-tile area
 };
 
-__device__ __forceinline__ Block block_of(int chunks_per_img) {
+__device__ __forceinline__ Work work_of(uint8_t* scratch, const ipp_ccl_work& w) {
+    Work k;
+    k.lab16 = reinterpret_cast<uint16_t*>(scratch + w.lab_off);
+    k.P = reinterpret_cast<int32_t*>(scratch + w.p_off);
+    k.A = reinterpret_cast<uint32_t*>(scratch + w.a_off);
+    k.entL = reinterpret_cast<int32_t*>(scratch + w.ent_off);
+    k.entA = reinterpret_cast<uint32_t*>(scratch + w.ent_off) + w.ent_cap;
+    return k;
+}
+
+// Foreground source: α > 1 of a 4-channel image, or the HSV mask of a
+// 3-channel BGR image (fused chain).
+enum { SRC_ALPHA = 0, SRC_HSV = 1 };
+
+template <int SRC, int NR, bool ZONES>
+__global__ void __launch_bounds__(256)
+k_ccl_tile(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
+           const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, int32_t* __restrict__ counts,
+           int tiles_per_img, int tiles_x_max, ipp_hsv_params hp) {
+    __shared__ int lab[TPX];
+    __shared__ uint32_t area[TPX];
+    __shared__ int32_t sdiv[SRC == SRC_HSV ? 256 : 1], hdiv[SRC == SRC_HSV ? 256 : 1];
+    __shared__ int nroots, base;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    Block r;
-    r.im = (int)(b / chunks_per_img);
-    r.base = (int64_t)(b - (uint32_t)r.im * chunks_per_img) * CHUNK;
-    return r;
-}
+    const int im = b / tiles_per_img;
+    const int t = b - im * tiles_per_img;
+    const int ty = t / tiles_x_max, tx = t - ty * tiles_x_max;
+    const ipp_image_desc d = descs[im];
+    const Frame f = frame_of(d);
+    if (tx >= f.tiles_x || ty >= f.tiles_y) return;  // block-uniform
+    const Work k = work_of(scratch, works[im]);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = tx * TW + lane;
 
-__device__ __forceinline__ bool is_fg(const uint8_t* img, const ipp_image_desc& d, int x, int y) {
-    return x < d.w && y < d.h && img[d.off + (int64_t)y * d.pitch + 4 * (int64_t)x + 3] > 1;
-}
-
-__global__ void __launch_bounds__(256)
-k_ccl_init(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs, int chunks,
-           int32_t* __restrict__ labels, const int64_t* __restrict__ lab_off, uint32_t* __restrict__ area) {
-    const Block bk = block_of(chunks);
-    const ipp_image_desc d = descs[bk.im];
-    const Geo g = geo_of(d);
-    int32_t* P = labels + lab_off[bk.im];
-    uint32_t* A = area + lab_off[bk.im];
-    for (int k = 0; k < 4; ++k) {
-        const int64_t L = bk.base + threadIdx.x + 256 * k;
-        if (L >= g.size) break;
-        int x, y;
-        decode(g, L, x, y);
-        P[L] = is_fg(img, d, x, y) ? (int32_t)L : -1;
-        A[L] = 0u;
+    Ranges<SRC == SRC_HSV ? NR : 1> R;
+    if (SRC == SRC_HSV) {
+        sdiv[threadIdx.x] = kSdiv[threadIdx.x];
+        hdiv[threadIdx.x] = kHdiv180[threadIdx.x];
+        ranges_init<SRC == SRC_HSV ? NR : 1, ZONES>(R, hp, d.w, d.h);
     }
-}
+    if (threadIdx.x == 0) nroots = 0;
+    __syncthreads();
 
-__global__ void __launch_bounds__(256)
-k_ccl_merge(const ipp_image_desc* __restrict__ descs, int chunks, int32_t* __restrict__ labels,
-            const int64_t* __restrict__ lab_off) {
-    const Block bk = block_of(chunks);
-    const ipp_image_desc d = descs[bk.im];
-    const Geo g = geo_of(d);
-    int32_t* P = labels + lab_off[bk.im];
-    for (int k = 0; k < 4; ++k) {
-        const int64_t L = bk.base + threadIdx.x + 256 * k;
-        if (L >= g.size) break;
-        if (ld(P + L) < 0) continue;
-        int x, y;
-        decode(g, L, x, y);
-        // 8-connectivity: left, up-left, up, up-right (each pair once)
-        const int nx[4] = {x - 1, x - 1, x, x + 1};
-        const int ny[4] = {y, y - 1, y - 1, y - 1};
+    uint32_t fgmask = 0;  // bit k: pixel (lane, wave + 4k) is foreground
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (nx[j] < 0 || ny[j] < 0 || nx[j] >= g.w) continue;
-            const int32_t q = encode(g, nx[j], ny[j]);
-            if (ld(P + q) >= 0) unite(P, (int32_t)L, q);
+    for (int j = 0; j < TH / 4; ++j) {
+        const int ly = wave + 4 * j, y = ty * TH + ly;
+        bool fg = false;
+        if (x < d.w && y < d.h) {
+            const uint8_t* row = img + d.off + (int64_t)y * d.pitch;
+            if (SRC == SRC_ALPHA) {
+                fg = row[4 * x + 3] > 1;
+            } else {
+                const bool wide_ok = (y < d.h - 1) || (x < d.w - 1);
+                const uint32_t px = load_rgb_opaque(row + 3 * x, wide_ok);
+                fg = hsv_keep<SRC == SRC_HSV ? NR : 1, ZONES, true>(R, sdiv, hdiv, px, x, y) != 0u;
+            }
+        }
+        const int li = lidx(lane, ly);
+        lab[li] = fg ? li : -1;
+        area[li] = 0u;
+        fgmask |= (fg ? 1u : 0u) << j;
+    }
+    __syncthreads();
+
+    // In-tile unions: left, up-left, up, up-right.
+#pragma unroll
+    for (int j = 0; j < TH / 4; ++j) {
+        if (!((fgmask >> j) & 1u)) continue;
+        const int ly = wave + 4 * j, li = lidx(lane, ly);
+        if (lane > 0 && lab[lidx(lane - 1, ly)] >= 0) lunite(lab, li, lidx(lane - 1, ly));
+        if (ly > 0) {
+            if (lane > 0 && lab[lidx(lane - 1, ly - 1)] >= 0) lunite(lab, li, lidx(lane - 1, ly - 1));
+            if (lab[lidx(lane, ly - 1)] >= 0) lunite(lab, li, lidx(lane, ly - 1));
+            if (lane < TW - 1 && lab[lidx(lane + 1, ly - 1)] >= 0) lunite(lab, li, lidx(lane + 1, ly - 1));
+        }
+    }
+    __syncthreads();
+
+    // Local roots per pixel → lab16 (raster, coalesced 2-B stores); areas.
+#pragma unroll
+    for (int j = 0; j < TH / 4; ++j) {
+        const int ly = wave + 4 * j, y = ty * TH + ly;
+        const bool fg = (fgmask >> j) & 1u;
+        int r = -1;
+        if (fg) {
+            r = lfind(lab, lidx(lane, ly));
+            atomicAdd(&area[r], 1u);
+        }
+        if (x < d.w && y < d.h) k.lab16[(int64_t)y * d.w + x] = fg ? (uint16_t)r : NOFG;
+    }
+    __syncthreads();
+
+    // One entry per local component (its root is the pixel with lab == itself).
+    int slot[TH / 4];
+#pragma unroll
+    for (int j = 0; j < TH / 4; ++j) {
+        slot[j] = -1;
+        const int li = lidx(lane, wave + 4 * j);
+        if (((fgmask >> j) & 1u) && lab[li] == li) slot[j] = atomicAdd(&nroots, 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && nroots > 0) base = atomicAdd(&counts[im], nroots);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TH / 4; ++j) {
+        if (slot[j] < 0) continue;
+        const int ly = wave + 4 * j, li = lidx(lane, ly);
+        const int32_t L = gidx(f, x, ty * TH + ly);
+        k.entL[base + slot[j]] = L;
+        k.entA[base + slot[j]] = area[li];
+        k.P[L] = L;
+        k.A[L] = 0u;
+    }
+}
+
+// Pixel (x, y) of tile-local root → global root index, or -1 for background.
+__device__ __forceinline__ int32_t root_of(const Frame& f, const Work& k, int x, int y) {
+    const uint16_t r = k.lab16[(int64_t)y * f.w + x];
+    if (r == NOFG) return -1;
+    return root_gidx(f, x / TW, y / TH, r);
+}
+
+// Border pairs: thread i < vert handles left pixel (64*bx - 1, y) of a
+// vertical tile border against (64*bx, y-1..y+1); the rest handle the upper
+// pixel (x, 32*by - 1) of a horizontal border against (x-1..x+1, 32*by).
+__global__ void __launch_bounds__(256)
+k_ccl_border(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
+             uint8_t* __restrict__ scratch, int chunks) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / chunks;
+    const int64_t i = (int64_t)(b - (uint32_t)im * chunks) * 256 + threadIdx.x;
+    const ipp_image_desc d = descs[im];
+    const Frame f = frame_of(d);
+    const Work k = work_of(scratch, works[im]);
+    const int64_t vert = (int64_t)(f.tiles_x - 1) * f.h;
+    const int64_t horz = (int64_t)(f.tiles_y - 1) * f.w;
+    if (i < vert) {
+        const int bx = 1 + (int)(i / f.h), y = (int)(i % f.h);
+        const int xl = bx * TW - 1;
+        const int32_t a = root_of(f, k, xl, y);
+        if (a < 0) return;
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int yy = y + dy;
+            if (yy < 0 || yy >= f.h) continue;
+            const int32_t c = root_of(f, k, xl + 1, yy);
+            if (c >= 0) gunite(k.P, a, c);
+        }
+    } else if (i < vert + horz) {
+        const int64_t j = i - vert;
+        const int by = 1 + (int)(j / f.w), x = (int)(j % f.w);
+        const int yu = by * TH - 1;
+        const int32_t a = root_of(f, k, x, yu);
+        if (a < 0) return;
+        for (int dx = -1; dx <= 1; ++dx) {
+            const int xx = x + dx;
+            if (xx < 0 || xx >= f.w) continue;
+            const int32_t c = root_of(f, k, xx, yu + 1);
+            if (c >= 0) gunite(k.P, a, c);
         }
     }
 }
 
 __global__ void __launch_bounds__(256)
-k_ccl_flatten_area(const ipp_image_desc* __restrict__ descs, int chunks, int32_t* __restrict__ labels,
-                   const int64_t* __restrict__ lab_off, uint32_t* __restrict__ area) {
-    const Block bk = block_of(chunks);
-    const ipp_image_desc d = descs[bk.im];
-    const Geo g = geo_of(d);
-    int32_t* P = labels + lab_off[bk.im];
-    uint32_t* A = area + lab_off[bk.im];
-    for (int k = 0; k < 4; ++k) {
-        const int64_t L = bk.base + threadIdx.x + 256 * k;
-        int32_t root = -1;
-        if (L < g.size && P[L] >= 0) {
-            root = find_root(P, (int32_t)L);
-            P[L] = root;
-        }
-        // wave-aggregated area histogram: one atomic per distinct root per wave
-        uint64_t pending = __ballot(root >= 0);
-        while (pending) {
-            const int leader = __ffsll((unsigned long long)pending) - 1;
-            const int32_t r = __shfl(root, leader);
-            const uint64_t same = __ballot(root == r) & pending;
-            if ((int)(threadIdx.x & 63) == leader) atomicAdd(A + r, (uint32_t)__popcll(same));
-            pending &= ~same;
-        }
-    }
+k_ccl_resolve(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch,
+              const int32_t* __restrict__ counts, int chunks) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / chunks;
+    const int e = (int)(b - (uint32_t)im * chunks) * 256 + threadIdx.x;
+    if (e >= counts[im]) return;
+    const Work k = work_of(scratch, works[im]);
+    const int32_t L = k.entL[e];
+    const int32_t R = gfind(k.P, L);
+    atomicAdd(k.A + R, k.entA[e]);
+    if (R != L) __hip_atomic_store(k.P + L, R, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(256)
-k_ccl_best(const ipp_image_desc* __restrict__ descs, int chunks, const int32_t* __restrict__ labels,
-           const int64_t* __restrict__ lab_off, const uint32_t* __restrict__ area,
-           unsigned long long* __restrict__ best) {
-    const Block bk = block_of(chunks);
-    const ipp_image_desc d = descs[bk.im];
-    const Geo g = geo_of(d);
-    const int32_t* P = labels + lab_off[bk.im];
-    const uint32_t* A = area + lab_off[bk.im];
+k_ccl_best(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, const int32_t* __restrict__ counts,
+           unsigned long long* __restrict__ best, int chunks) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / chunks;
+    const int e = (int)(b - (uint32_t)im * chunks) * 256 + threadIdx.x;
     unsigned long long key = 0ull;
-    for (int k = 0; k < 4; ++k) {
-        const int64_t L = bk.base + threadIdx.x + 256 * k;
-        if (L < g.size && P[L] == (int32_t)L) {
-            const unsigned long long kk =
-                ((unsigned long long)A[L] << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)L);
-            key = kk > key ? kk : key;
-        }
+    if (e < counts[im]) {
+        const Work k = work_of(scratch, works[im]);
+        const int32_t L = k.entL[e];
+        if (k.P[L] == L)
+            key = ((unsigned long long)k.A[L] << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)L);
     }
     for (int off = 32; off > 0; off >>= 1) {
         const unsigned long long o = __shfl_xor(key, off);
         key = o > key ? o : key;
     }
-    if ((threadIdx.x & 63) == 0 && key) atomicMax(best + bk.im, key);
+    if ((threadIdx.x & 63) == 0 && key) atomicMax(best + im, key);
 }
 
+__device__ __forceinline__ int32_t best_root(unsigned long long key) {
+    return key ? (int32_t)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull)) : -1;
+}
+
+// bbox of the best component: rows of 64-pixel segments, wave min/max, then
+// four device atomics per wave.
 __global__ void __launch_bounds__(256)
-k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs, int chunks,
-            const int32_t* __restrict__ labels, const int64_t* __restrict__ lab_off,
-            const unsigned long long* __restrict__ best, int32_t* __restrict__ bbox) {
-    const Block bk = block_of(chunks);
-    const ipp_image_desc d = descs[bk.im];
-    const Geo g = geo_of(d);
-    const int32_t* P = labels + lab_off[bk.im];
-    const unsigned long long bkey = best[bk.im];
-    const int32_t broot = (int32_t)(0xFFFFFFFFu - (uint32_t)(bkey & 0xFFFFFFFFull));
+k_ccl_bbox(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
+           uint8_t* __restrict__ scratch, const unsigned long long* __restrict__ best, int32_t* __restrict__ bbox,
+           int tiles_per_img, int tiles_x_max) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / tiles_per_img;
+    const int t = b - im * tiles_per_img;
+    const int ty = t / tiles_x_max, tx = t - ty * tiles_x_max;
+    const ipp_image_desc d = descs[im];
+    const Frame f = frame_of(d);
+    if (tx >= f.tiles_x || ty >= f.tiles_y) return;
+    const int32_t broot = best_root(best[im]);
+    if (broot < 0) return;
+    const Work k = work_of(scratch, works[im]);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = tx * TW + lane;
     int xmin = INT32_MAX, ymin = INT32_MAX, xmax = -1, ymax = -1;
-    for (int k = 0; k < 4; ++k) {
-        const int64_t L = bk.base + threadIdx.x + 256 * k;
-        if (L >= g.size) break;
-        int x, y;
-        decode(g, L, x, y);
-        if (x >= g.w || y >= g.h) continue;
-        uint8_t* a = img + d.off + (int64_t)y * d.pitch + 4 * (int64_t)x + 3;
-        uint8_t av = *a;
-        if (bkey != 0ull && P[L] != broot && av != 0) {
-            av = 0;
-            *a = 0;
-        }
-        if (av != 0) {
-            xmin = min(xmin, x);
-            xmax = max(xmax, x);
-            ymin = min(ymin, y);
-            ymax = max(ymax, y);
+    if (x < d.w) {
+        for (int j = 0; j < TH / 4; ++j) {
+            const int y = ty * TH + wave + 4 * j;
+            if (y >= d.h) break;
+            const int32_t r = root_of(f, k, x, y);
+            if (r >= 0 && k.P[r] == broot) {
+                xmin = min(xmin, x);
+                xmax = max(xmax, x);
+                ymin = min(ymin, y);
+                ymax = max(ymax, y);
+            }
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -230,15 +382,77 @@ k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
         xmax = max(xmax, __shfl_xor(xmax, off));
         ymax = max(ymax, __shfl_xor(ymax, off));
     }
-    if ((threadIdx.x & 63) == 0 && xmax >= 0) {
-        atomicMin(&bbox[4 * bk.im + 0], xmin);
-        atomicMin(&bbox[4 * bk.im + 1], ymin);
-        atomicMax(&bbox[4 * bk.im + 2], xmax + 1);
-        atomicMax(&bbox[4 * bk.im + 3], ymax + 1);
+    if (lane == 0 && xmax >= 0) {
+        atomicMin(&bbox[4 * im + 0], xmin);
+        atomicMin(&bbox[4 * im + 1], ymin);
+        atomicMax(&bbox[4 * im + 2], xmax + 1);
+        atomicMax(&bbox[4 * im + 3], ymax + 1);
     }
 }
 
-__global__ void k_ccl_prep(int32_t* bbox, unsigned long long* best, int n) {
+// K6, plugin path: in place on a 4-channel image, α := 0 outside the best
+// component (images without any component are left unchanged).
+__global__ void __launch_bounds__(256)
+k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
+            uint8_t* __restrict__ scratch, const unsigned long long* __restrict__ best, int tiles_per_img,
+            int tiles_x_max) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / tiles_per_img;
+    const int t = b - im * tiles_per_img;
+    const int ty = t / tiles_x_max, tx = t - ty * tiles_x_max;
+    const ipp_image_desc d = descs[im];
+    const Frame f = frame_of(d);
+    if (tx >= f.tiles_x || ty >= f.tiles_y) return;
+    const int32_t broot = best_root(best[im]);
+    if (broot < 0) return;
+    const Work k = work_of(scratch, works[im]);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = tx * TW + lane;
+    if (x >= d.w) return;
+    for (int j = 0; j < TH / 4; ++j) {
+        const int y = ty * TH + wave + 4 * j;
+        if (y >= d.h) break;
+        const int32_t r = root_of(f, k, x, y);
+        if (r < 0 || k.P[r] != broot) {
+            uint8_t* a = img + d.off + (int64_t)y * d.pitch + 4 * (int64_t)x + 3;
+            if (*a) *a = 0;
+        }
+    }
+}
+
+// K6, fused chain: crop-fit of the BGR frame to the best component's bbox,
+// written as BGRA (α = 255 inside the component, 0 elsewhere) into the image's
+// output slot.  Each thread owns one output pixel of a 64×4 block tile.
+__global__ void __launch_bounds__(256)
+k_ccl_crop_bgr(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
+               const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch,
+               const unsigned long long* __restrict__ best, const int32_t* __restrict__ bbox,
+               uint8_t* __restrict__ out, const ipp_image_desc* __restrict__ out_descs, int tiles_x, int tiles_y) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int per_img = tiles_x * tiles_y;
+    const int im = b / per_img;
+    const int t = b - im * per_img;
+    const int ty = t / tiles_x, tx = t - ty * tiles_x;
+    const int32_t broot = best_root(best[im]);
+    if (broot < 0) return;
+    const int x0 = bbox[4 * im + 0], y0 = bbox[4 * im + 1];
+    const int cw = bbox[4 * im + 2] - x0, chh = bbox[4 * im + 3] - y0;
+    const int ox = tx * 64 + (int)(threadIdx.x & 63), oy = ty * 4 + (int)(threadIdx.x >> 6);
+    if (ox >= cw || oy >= chh) return;
+    const ipp_image_desc d = descs[im];
+    const ipp_image_desc od = out_descs[im];
+    const Frame f = frame_of(d);
+    const Work k = work_of(scratch, works[im]);
+    const int x = x0 + ox, y = y0 + oy;
+    const bool wide_ok = (y < d.h - 1) || (x < d.w - 1);
+    const uint32_t px = load_rgb_opaque(img + d.off + (int64_t)y * d.pitch + 3 * (int64_t)x, wide_ok);
+    const int32_t r = root_of(f, k, x, y);
+    const bool in = r >= 0 && k.P[r] == broot;
+    reinterpret_cast<uint32_t*>(out + od.off + (int64_t)oy * od.pitch)[ox] =
+        (px & 0x00FFFFFFu) | (in ? 0xFF000000u : 0u);
+}
+
+__global__ void k_ccl_prep(int32_t* bbox, unsigned long long* best, int32_t* counts, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
         bbox[4 * i + 0] = INT32_MAX;
@@ -246,42 +460,136 @@ __global__ void k_ccl_prep(int32_t* bbox, unsigned long long* best, int n) {
         bbox[4 * i + 2] = -1;
         bbox[4 * i + 3] = -1;
         best[i] = 0ull;
+        counts[i] = 0;
     }
 }
 
 __global__ void k_ccl_finish(int32_t* bbox, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && bbox[4 * i + 2] < 0) bbox[4 * i + 0] = bbox[4 * i + 1] = -1;
+    if (i < n && bbox[4 * i + 2] < 0) bbox[4 * i + 0] = bbox[4 * i + 1] = bbox[4 * i + 2] = bbox[4 * i + 3] = -1;
+}
+
+struct Launch {
+    int tiles_x, tiles_y, tiles_per_img;
+    int border_chunks, ent_chunks;
+    dim3 tile_grid, border_grid, ent_grid;
+    bool ok;
+};
+
+Launch plan_launch(int n, int max_w, int max_h, int64_t max_ent) {
+    Launch L{};
+    L.tiles_x = (max_w + TW - 1) / TW;
+    L.tiles_y = (max_h + TH - 1) / TH;
+    L.tiles_per_img = L.tiles_x * L.tiles_y;
+    const int64_t border = (int64_t)(L.tiles_x - 1) * max_h + (int64_t)(L.tiles_y - 1) * max_w;
+    L.border_chunks = (int)std::max<int64_t>(1, (border + 255) / 256);
+    L.ent_chunks = (int)std::max<int64_t>(1, (max_ent + 255) / 256);
+    const int64_t tb = (int64_t)L.tiles_per_img * n, bb = (int64_t)L.border_chunks * n, eb = (int64_t)L.ent_chunks * n;
+    L.ok = tb < INT32_MAX && bb < INT32_MAX && eb < INT32_MAX;
+    L.tile_grid = dim3((uint32_t)tb);
+    L.border_grid = dim3((uint32_t)bb);
+    L.ent_grid = dim3((uint32_t)eb);
+    return L;
+}
+
+template <int SRC, int NR, bool ZONES>
+void launch_tiles(const Launch& L, hipStream_t s, const uint8_t* img, const ipp_image_desc* descs,
+                  const ipp_ccl_work* works, uint8_t* scratch, int32_t* counts, const ipp_hsv_params& hp) {
+    hipLaunchKernelGGL((k_ccl_tile<SRC, NR, ZONES>), L.tile_grid, dim3(256), 0, s, img, descs, works, scratch, counts,
+                       L.tiles_per_img, L.tiles_x, hp);
+}
+
+// K1..K5 common to both entry points.
+int run_labels(int src, const uint8_t* img, const ipp_image_desc* descs, int32_t n, int32_t max_w, int32_t max_h,
+               const ipp_hsv_params* hsv, const ipp_ccl_work* works, uint8_t* scratch, int64_t max_ent,
+               int32_t* counts, unsigned long long* best, int32_t* bbox, hipStream_t s, Launch& L) {
+    L = plan_launch(n, max_w, max_h, max_ent);
+    if (!L.ok) return IPP_E_ARG;
+    const int nb = (n + 255) / 256;
+    hipLaunchKernelGGL(k_ccl_prep, dim3(nb), dim3(256), 0, s, bbox, best, counts, n);
+    if (src == SRC_ALPHA) {
+        launch_tiles<SRC_ALPHA, 1, false>(L, s, img, descs, works, scratch, counts, ipp_hsv_params{});
+    } else {
+        const bool zones = hsv_has_zones(*hsv);
+        const bool small = hsv->n_ranges <= 4;
+        const ipp_hsv_params q = hsv_pad(*hsv, small ? 4 : IPP_MAX_HSV_RANGES);
+        if (small && !zones) launch_tiles<SRC_HSV, 4, false>(L, s, img, descs, works, scratch, counts, q);
+        else if (small) launch_tiles<SRC_HSV, 4, true>(L, s, img, descs, works, scratch, counts, q);
+        else if (!zones) launch_tiles<SRC_HSV, IPP_MAX_HSV_RANGES, false>(L, s, img, descs, works, scratch, counts, q);
+        else launch_tiles<SRC_HSV, IPP_MAX_HSV_RANGES, true>(L, s, img, descs, works, scratch, counts, q);
+    }
+    hipLaunchKernelGGL(k_ccl_border, L.border_grid, dim3(256), 0, s, descs, works, scratch, L.border_chunks);
+    hipLaunchKernelGGL(k_ccl_resolve, L.ent_grid, dim3(256), 0, s, works, scratch, counts, L.ent_chunks);
+    hipLaunchKernelGGL(k_ccl_best, L.ent_grid, dim3(256), 0, s, works, scratch, counts, best, L.ent_chunks);
+    hipLaunchKernelGGL(k_ccl_bbox, L.tile_grid, dim3(256), 0, s, descs, works, scratch, best, bbox, L.tiles_per_img,
+                       L.tiles_x);
+    return IPP_OK;
 }
 
 }  // namespace
 
-// stats: caller scratch of n_images 64-bit words (best key per image:
-// area << 32 | ~root); labels/area: int32/uint32 scratch of
-// 4*ceil(w/2)*ceil(h/2) entries per image starting at lab_off[i].
+extern "C" int64_t ipp_ccl_scratch_layout(int32_t w, int32_t h, ipp_ccl_work* work) {
+    if (w <= 0 || h <= 0) return IPP_E_ARG;
+    const int64_t wb = (w + 1) / 2, hb = (h + 1) / 2;
+    const int64_t slots = 4 * wb * hb;
+    if (slots >= INT32_MAX) return IPP_E_RANGE;
+    // ≤ one component per 2×2 block of a tile (8-connectivity), per tile
+    const int64_t tiles = (int64_t)((w + TW - 1) / TW) * ((h + TH - 1) / TH);
+    const int64_t cap = tiles * (TPX / 4);
+    auto al = [](int64_t v) { return (v + 255) & ~(int64_t)255; };
+    ipp_ccl_work k{};
+    k.lab_off = 0;
+    k.p_off = al(2 * (int64_t)w * h);
+    k.a_off = k.p_off + al(4 * slots);
+    k.ent_off = k.a_off + al(4 * slots);
+    k.ent_cap = cap;
+    const int64_t total = k.ent_off + al(8 * cap);
+    if (work) *work = k;
+    return total;
+}
+
 extern "C" int ipp_ccl_keep_largest(uint8_t* img, const ipp_image_desc* descs, int32_t n_images, int32_t max_w,
-                                    int32_t max_h, int32_t* labels, const int64_t* lab_off, uint32_t* area,
-                                    int64_t* stats, int32_t* bbox, void* stream) {
+                                    int32_t max_h, const ipp_ccl_work* works, uint8_t* scratch, int64_t max_ent,
+                                    int32_t* counts, int64_t* stats, int32_t* bbox, void* stream) {
     if (n_images == 0) return IPP_OK;
-    if (!img || !descs || !labels || !lab_off || !area || !stats || !bbox || n_images < 0 || max_w <= 0 ||
-        max_h <= 0)
+    if (!img || !descs || !works || !scratch || !counts || !stats || !bbox || n_images < 0 || max_w <= 0 ||
+        max_h <= 0 || max_ent <= 0)
         return IPP_E_ARG;
-    const int64_t size = 4ll * ((max_w + 1) / 2) * ((max_h + 1) / 2);
-    if (size >= INT32_MAX) return IPP_E_RANGE;
-    const int chunks = (int)((size + CHUNK - 1) / CHUNK);
-    const int64_t blocks = (int64_t)chunks * n_images;
-    if (blocks >= INT32_MAX) return IPP_E_ARG;
     hipStream_t s = (hipStream_t)stream;
     unsigned long long* best = reinterpret_cast<unsigned long long*>(stats);
-    const int nb = (n_images + 255) / 256;
-    const dim3 grid((uint32_t)blocks), blk(256);
-    hipLaunchKernelGGL(k_ccl_prep, dim3(nb), blk, 0, s, bbox, best, n_images);
-    hipLaunchKernelGGL(k_ccl_init, grid, blk, 0, s, img, descs, chunks, labels, lab_off, area);
-    hipLaunchKernelGGL(k_ccl_merge, grid, blk, 0, s, descs, chunks, labels, lab_off);
-    hipLaunchKernelGGL(k_ccl_flatten_area, grid, blk, 0, s, descs, chunks, labels, lab_off, area);
-    hipLaunchKernelGGL(k_ccl_best, grid, blk, 0, s, descs, chunks, labels, lab_off, area, best);
-    hipLaunchKernelGGL(k_ccl_apply, grid, blk, 0, s, img, descs, chunks, labels, lab_off, best, bbox);
-    hipLaunchKernelGGL(k_ccl_finish, dim3(nb), blk, 0, s, bbox, n_images);
+    Launch L;
+    const int rc = run_labels(SRC_ALPHA, img, descs, n_images, max_w, max_h, nullptr, works, scratch, max_ent, counts,
+                              best, bbox, s, L);
+    if (rc != IPP_OK) return rc;
+    hipLaunchKernelGGL(k_ccl_apply, L.tile_grid, dim3(256), 0, s, img, descs, works, scratch, best, L.tiles_per_img,
+                       L.tiles_x);
+    hipLaunchKernelGGL(k_ccl_finish, dim3((n_images + 255) / 256), dim3(256), 0, s, bbox, n_images);
+    IPP_CHECK_LAUNCH();
+    return IPP_OK;
+}
+
+extern "C" int ipp_video_keep_largest(const uint8_t* frames, const ipp_image_desc* descs, int32_t n_images,
+                                      int32_t max_w, int32_t max_h, const ipp_hsv_params* hsv,
+                                      const ipp_ccl_work* works, uint8_t* scratch, int64_t max_ent, int32_t* counts,
+                                      int64_t* stats, int32_t* bbox, uint8_t* out,
+                                      const ipp_image_desc* out_descs, void* stream) {
+    if (n_images == 0) return IPP_OK;
+    if (!frames || !descs || !hsv || !works || !scratch || !counts || !stats || !bbox || !out || !out_descs ||
+        n_images < 0 || max_w <= 0 || max_h <= 0 || max_ent <= 0)
+        return IPP_E_ARG;
+    if (hsv->n_ranges < 0 || hsv->n_ranges > IPP_MAX_HSV_RANGES) return IPP_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long* best = reinterpret_cast<unsigned long long*>(stats);
+    Launch L;
+    const int rc = run_labels(SRC_HSV, frames, descs, n_images, max_w, max_h, hsv, works, scratch, max_ent, counts,
+                              best, bbox, s, L);
+    if (rc != IPP_OK) return rc;
+    const int tx = (max_w + 63) / 64, ty = (max_h + 3) / 4;
+    const int64_t blocks = (int64_t)tx * ty * n_images;
+    if (blocks >= INT32_MAX) return IPP_E_ARG;
+    hipLaunchKernelGGL(k_ccl_crop_bgr, dim3((uint32_t)blocks), dim3(256), 0, s, frames, descs, works, scratch, best,
+                       bbox, out, out_descs, tx, ty);
+    hipLaunchKernelGGL(k_ccl_finish, dim3((n_images + 255) / 256), dim3(256), 0, s, bbox, n_images);
     IPP_CHECK_LAUNCH();
     return IPP_OK;
 }

@@ -71,30 +71,55 @@ k_rotate_flip_nearest(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst
     }
 }
 
-// Window copy with optional mirror, any bytes-per-pixel (1..4).
+// Window copy with optional mirror, any bytes-per-pixel (1..4).  Each thread
+// owns 16 bytes of one output row (a block covers 4 rows × 1 KiB): rows that
+// are not mirrored in x are contiguous byte runs, copied with 4 unaligned
+// dword loads and one 16-B store; mirrored rows take a per-byte path.  With
+// FROM_BBOX the window is read from a device bbox array (x0, y0, x1, y1) per
+// image — the crop-fit of pixels_isolés.py:74-81 without a host round trip;
+// an empty bbox (x0 < 0) copies nothing.
+template <bool FROM_BBOX>
 __global__ void __launch_bounds__(256)
-k_copy_window(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-              const ipp_copy_desc* __restrict__ descs, int tiles_x, int tiles_y) {
+k_copy_rows(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, const ipp_copy_desc* __restrict__ descs,
+            const int32_t* __restrict__ bbox, int tiles_x, int tiles_y) {
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int per_img = tiles_x * tiles_y;
     const int img = b / per_img;
     const int t = b - img * per_img;
     const int ty = t / tiles_x, tx = t - ty * tiles_x;
     const ipp_copy_desc d = descs[img];
-    const int y = ty * TILE_H + (int)(threadIdx.x >> 4);
-    const int x0 = tx * TILE_W + (int)(threadIdx.x & 15) * PX_PER_THREAD;
-    if (y >= d.h || x0 >= d.w) return;
-    const int sy = d.y0 + ((d.flip & 2) ? d.h - 1 - y : y);
-    const uint8_t* s = src + d.src_off + (int64_t)sy * d.src_pitch;
-    uint8_t* o = dst + d.dst_off + (int64_t)y * d.dst_pitch;
-    for (int k = 0; k < PX_PER_THREAD; ++k) {
-        const int x = x0 + k;
-        if (x >= d.w) break;
-        const int sx = d.x0 + ((d.flip & 1) ? d.w - 1 - x : x);
-        const uint8_t* sp = s + (int64_t)sx * d.cn;
-        uint8_t* op = o + (int64_t)x * d.cn;
-        for (int c = 0; c < d.cn; ++c) op[c] = sp[c];
+    int x0 = d.x0, y0 = d.y0, w = d.w, h = d.h;
+    if (FROM_BBOX) {
+        x0 = bbox[4 * img + 0];
+        y0 = bbox[4 * img + 1];
+        w = bbox[4 * img + 2] - x0;
+        h = bbox[4 * img + 3] - y0;
+        if (x0 < 0) return;
     }
+    const int y = ty * 4 + (int)(threadIdx.x >> 6);
+    const int c0 = (tx * 64 + (int)(threadIdx.x & 63)) * 16;
+    const int row_bytes = w * d.cn;
+    if (y >= h || c0 >= row_bytes) return;
+    const int sy = y0 + ((d.flip & 2) ? h - 1 - y : y);
+    const uint8_t* s = src + d.src_off + (int64_t)sy * d.src_pitch + (int64_t)x0 * d.cn;
+    uint8_t* o = dst + d.dst_off + (int64_t)y * d.dst_pitch + c0;
+    const int n = min(16, row_bytes - c0);
+    uint32_t wv[4] = {0u, 0u, 0u, 0u};
+    if (!(d.flip & 1)) {
+        if (n == 16) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) wv[k] = ld_u32_unaligned(s + c0 + 4 * k);
+        } else {
+            for (int j = 0; j < n; ++j) wv[j >> 2] |= (uint32_t)s[c0 + j] << (8 * (j & 3));
+        }
+    } else {
+        for (int j = 0; j < n; ++j) {
+            const int bi = c0 + j, px = bi / d.cn, ch = bi - px * d.cn;
+            wv[j >> 2] |= (uint32_t)s[(int64_t)(w - 1 - px) * d.cn + ch] << (8 * (j & 3));
+        }
+    }
+    const bool vec = n == 16 && (reinterpret_cast<uintptr_t>(o) & 15u) == 0;
+    store16(o, n, vec, wv);
 }
 
 // Bounding box of non-zero pixels (Pillow getbbox(alpha_only=True): the alpha
@@ -187,11 +212,27 @@ extern "C" int ipp_copy_window(const uint8_t* src, uint8_t* dst, const ipp_copy_
                                int32_t max_w, int32_t max_h, void* stream) {
     if (n_images == 0) return IPP_OK;
     if (!src || !dst || !descs || n_images < 0 || max_w <= 0 || max_h <= 0) return IPP_E_ARG;
-    const int tx = (max_w + TILE_W - 1) / TILE_W, ty = (max_h + TILE_H - 1) / TILE_H;
+    // max_w is in pixels; size the grid for 4 bytes per pixel (threads past a
+    // row's bytes exit)
+    const int tx = (max_w * 4 + 1023) / 1024, ty = (max_h + 3) / 4;
     const int64_t blocks = (int64_t)tx * ty * n_images;
     if (!grid_ok(blocks)) return IPP_E_ARG;
-    hipLaunchKernelGGL(k_copy_window, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, src, dst, descs,
-                       tx, ty);
+    hipLaunchKernelGGL(k_copy_rows<false>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, src, dst,
+                       descs, nullptr, tx, ty);
+    IPP_CHECK_LAUNCH();
+    return IPP_OK;
+}
+
+extern "C" int ipp_crop_to_bbox(const uint8_t* src, uint8_t* dst, const ipp_copy_desc* descs, const int32_t* bbox,
+                                int32_t n_images, int32_t max_w, int32_t max_h, int32_t cn, void* stream) {
+    if (n_images == 0) return IPP_OK;
+    if (!src || !dst || !descs || !bbox || n_images < 0 || max_w <= 0 || max_h <= 0 || cn < 1 || cn > 4)
+        return IPP_E_ARG;
+    const int tx = (max_w * cn + 1023) / 1024, ty = (max_h + 3) / 4;
+    const int64_t blocks = (int64_t)tx * ty * n_images;
+    if (!grid_ok(blocks)) return IPP_E_ARG;
+    hipLaunchKernelGGL(k_copy_rows<true>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, src, dst, descs,
+                       bbox, tx, ty);
     IPP_CHECK_LAUNCH();
     return IPP_OK;
 }

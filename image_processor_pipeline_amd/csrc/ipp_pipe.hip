@@ -25,9 +25,10 @@
 
 namespace {
 
-constexpr int HX = 64;            // H-pass outputs per block (one per lane)
+constexpr int HX = 64;            // H-pass outputs per chunk (one per lane)
 constexpr int HR = 16;            // H-pass rows per block (4 per thread)
-constexpr int WSTRIDE = 400;      // LDS bytes per plane row (≡ 4 dwords mod 32 banks)
+constexpr int RING = 512;         // window ring: M columns x live at x & (RING - 1)
+constexpr int WSTRIDE = 528;      // LDS bytes per plane row (≡ 4 dwords mod 32 banks)
 constexpr int VR = 4;             // composite rows per vblend block
 
 __device__ __forceinline__ int32_t sdot4(uint32_t a, uint32_t b, int32_t c) {
@@ -46,88 +47,6 @@ __device__ __forceinline__ int32_t sdot4(uint32_t a, uint32_t b, int32_t c) {
 
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
     return __builtin_amdgcn_perm(hi, lo, sel);
-}
-
-// 24-bit multiply-add, exact for the HSV table products (|a| < 2^11,
-// |b| < 2^21, result < 2^31).  Written as VOP3 so the compiler cannot widen it
-// to the quarter-rate v_mad_u64_u32 it otherwise picks for this pattern.
-__device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t d;
-    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
-}
-__device__ __forceinline__ int32_t mad_i24(int32_t a, int32_t b, int32_t c) {
-    int32_t d;
-    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
-}
-
-// Per-block uniform HSV range state (SGPRs).  (h, s, v) are packed as 10-bit
-// fields X0 = h | s << 10 | v << 20; with guard bits G at 9/19/29,
-//   (X0|G) - lo  keeps field guard f  ⟺  x_f >= lo_f,
-//   (hi|G) - X0  keeps field guard f  ⟺  x_f <= hi_f,
-// so a range holds iff every guard survives both subtractions (no borrow can
-// cross a field: x_f, lo_f, hi_f <= 255 < 512).
-constexpr uint32_t kGuard = (1u << 9) | (1u << 19) | (1u << 29);
-
-template <int NR>
-struct Ranges {
-    uint32_t lo[NR], hig[NR];
-    int32_t r0[NR], rh[NR], c0[NR], cw[NR];
-};
-
-template <int NR, bool ZONES>
-__device__ __forceinline__ void ranges_init(Ranges<NR>& R, const ipp_hsv_params& hp, int w, int h) {
-#pragma unroll
-    for (int k = 0; k < NR; ++k) {
-        const ipp_hsv_range& q = hp.r[k];
-        R.lo[k] = (uint32_t)q.lo[0] | ((uint32_t)q.lo[1] << 10) | ((uint32_t)q.lo[2] << 20);
-        R.hig[k] = ((uint32_t)q.hi[0] | ((uint32_t)q.hi[1] << 10) | ((uint32_t)q.hi[2] << 20)) | kGuard;
-        if (ZONES) {
-            int a, b, cc, dd;
-            slice_indices(q.zone[0], h - q.zone[1], h, a, b);
-            slice_indices(q.zone[2], w - q.zone[3], w, cc, dd);
-            R.r0[k] = a;
-            R.rh[k] = b - a;
-            R.c0[k] = cc;
-            R.cw[k] = dd - cc;
-        }
-    }
-}
-
-// OpenCV RGB2HSV_b (hsv_shift 12; sdiv/hdiv tables in LDS) + the union of
-// inRange boxes (and zones) → keep?
-template <int NR, bool ZONES>
-__device__ __forceinline__ uint32_t hsv_keep(const Ranges<NR>& R, const int32_t* sdiv_t, const int32_t* hdiv_t,
-                                         uint32_t px, int x, int y) {
-    const int r = px & 0xFF, g = (px >> 8) & 0xFF, b = (px >> 16) & 0xFF;  // Pillow order
-    const int v = max(max(b, g), r);
-    const int vmin = min(min(b, g), r);
-    const int diff = v - vmin;
-    const uint32_t sat = mad_u24((uint32_t)diff, (uint32_t)sdiv_t[v], 2048u) >> 12;
-    // branch-free hue numerator (OpenCV's vr/vg masks): v==r ? g-b : v==g ? b-r+2d : r-g+4d
-    const int h_r = g - b, h_g = b - r + 2 * diff, h_b = r - g + 4 * diff;
-    int hh = (v == g) ? h_g : h_b;
-    hh = (v == r) ? h_r : hh;
-    // h < 0 → h + 180, as min over unsigned (a negative h wraps above h + 180)
-    const uint32_t hu = (uint32_t)(mad_i24(hh, hdiv_t[diff], 2048) >> 12);
-    const uint32_t hp = min(hu, hu + 180u);
-    const uint32_t x0 = hp | (sat << 10) | ((uint32_t)v << 20);
-    const uint32_t xg = x0 | kGuard;
-    uint32_t nmin = 1u;  // 0 ⟺ some range contains the pixel, else 1
-#pragma unroll
-    for (int k = 0; k < NR; ++k) {
-        uint32_t n = ~((xg - R.lo[k]) & (R.hig[k] - x0)) & kGuard;
-        if (ZONES) n |= (((uint32_t)(y - R.r0[k]) < (uint32_t)R.rh[k]) & ((uint32_t)(x - R.c0[k]) < (uint32_t)R.cw[k])) ? 0u : 1u;
-        nmin = min(nmin, n);
-    }
-    return nmin;
-}
-
-// Opaque M pixel (alpha 255) when kept, else transparent black: 0 - keep is
-// the all-ones mask.
-__device__ __forceinline__ uint32_t keep_pixel(uint32_t p, uint32_t keep) {
-    return (p | 0xFF000000u) & (0u - keep);
 }
 
 // Source sampling for M pixel (x, y): flip + bbox offset folded into the 16.16
@@ -211,24 +130,27 @@ __device__ int32_t g_dbg_meta[8];
 #endif
 
 struct HpassLds {
-    uint8_t win[4][HR][WSTRIDE];      // planar window, bytes p ^ 0x80
+    uint8_t win[4][HR][WSTRIDE];      // planar window ring, bytes p ^ 0x80
     int32_t sdiv[256], hdiv[256];     // OpenCV RGB2HSV_b division tables
 };
 
+// One block = one 16-row band of one item, sweeping all its outputs in chunks
+// of ≤ 64.  The M window is a ring of RING columns: each chunk only computes
+// the columns its predecessor did not (consecutive chunks' windows overlap by
+// the filter support), so every M pixel of the band is gathered and
+// HSV-tested exactly once.
 template <int NR, bool ZONES, int CN>
 __global__ void __launch_bounds__(256)
 k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
-             const ipp_pipe_desc* __restrict__ descs, int tiles_x, int tiles_y, ipp_hsv_params hp) {
+             const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp) {
     __shared__ HpassLds L;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int per_img = tiles_x * tiles_y;
-    const int im = b / per_img;
-    const int t = b - im * per_img;
-    const int ty = t / tiles_x, tx = t - ty * tiles_x;
+    const int im = b / tiles_y;
+    const int ty = b - im * tiles_y;
     const ipp_gather_desc g = descs[im].g;
     const ipp_resample_desc h = descs[im].h;
-    const int xo0 = tx * HX, row0 = ty * HR;
-    if (xo0 >= h.out_len || row0 >= h.lines) return;  // block-uniform
+    const int row0 = ty * HR;
+    if (row0 >= h.lines) return;  // block-uniform
 
     for (int i = threadIdx.x; i < 256; i += 256) {
         L.sdiv[i] = kSdiv[i];
@@ -252,29 +174,29 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
     const uint32_t rowx = (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1;
     const uint32_t rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
 
-    // Outputs of this block: split into sub-chunks whose window fits WSTRIDE.
-    const int xo_end = min(xo0 + HX, h.out_len);
-    for (int s0 = xo0; s0 < xo_end;) {
-        int s1 = xo_end;
-        while (s1 - s0 > 1 && hdr[s1 - 1].x + 4 * ngs - hdr[s0].x > WSTRIDE) s1 = s0 + (s1 - s0 + 1) / 2;
-        const int W0 = hdr[s0].x;
-        const int ww = hdr[s1 - 1].x + 4 * ngs - W0;  // multiple of 4
-        const int ng4 = ww >> 2;
+    int filled = hdr[0].x;  // ring holds M columns [.., filled)
+    for (int s0 = 0; s0 < h.out_len;) {
+        int s1 = min(s0 + HX, h.out_len);
+        while (s1 - s0 > 1 && hdr[s1 - 1].x + 4 * ngs - hdr[s0].x > RING) s1 = s0 + (s1 - s0 + 1) / 2;
+        const int W1 = hdr[s1 - 1].x + 4 * ngs;   // window end (multiple of 4)
+        const int c0 = max(filled, hdr[s0].x);    // first column not in the ring
+        const int ng4 = max(0, (W1 - c0) >> 2);
+        filled = max(filled, W1);
 
-        if (s0 == xo0) __syncthreads();  // HSV tables visible
+        if (s0 == 0) __syncthreads();  // HSV tables visible
 
-        // Phase 1: M pixels of the window → planar LDS; next step's gathers
-        // are in flight while this step's HSV runs.
+        // Phase 1: new M columns → planar LDS ring; next step's gathers are in
+        // flight while this step's HSV runs.
         Gather4<CN> cur, nxt;
         int cg0 = wave * 4;
         if (cg0 < ng4) {
-            const int x = W0 + 4 * (cg0 + (lane & 3));
+            const int x = c0 + 4 * (cg0 + (lane & 3));
             gather4_issue<CN>(S, rowx + (uint32_t)x * (uint32_t)S.b0, rowy + (uint32_t)x * (uint32_t)S.b3, nxt);
         }
         for (; cg0 < ng4; cg0 += 16) {
             cur = nxt;
             const int cg = cg0 + (lane & 3);
-            const int x = W0 + 4 * cg;
+            const int x = c0 + 4 * cg;
             if (cg0 + 16 < ng4) {
                 const int xn = x + 64;
                 gather4_issue<CN>(S, rowx + (uint32_t)xn * (uint32_t)S.b0, rowy + (uint32_t)xn * (uint32_t)S.b3, nxt);
@@ -296,9 +218,10 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
             if (active) {
                 uint32_t ch[4];
                 transpose4(px[0], px[1], px[2], px[3], ch);
+                const int pos = x & (RING - 1);
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    *reinterpret_cast<uint32_t*>(&L.win[c][r][4 * cg]) = ch[c] ^ 0x80808080u;
+                    *reinterpret_cast<uint32_t*>(&L.win[c][r][pos]) = ch[c] ^ 0x80808080u;
             }
         }
         __syncthreads();
@@ -307,19 +230,18 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
         const int xo = s0 + lane;
         if (xo < s1) {
             const int4 hd = hdr[xo];
-            const int wo = hd.x - W0;
             int32_t acc[4][4][3];
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
                 for (int c = 0; c < 4; ++c) acc[rr][c][0] = acc[rr][c][1] = acc[rr][c][2] = 0;
-            auto step = [&](int j, const uint4 tp) {
+            auto step = [&](int pos, const uint4 tp) {
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     const int row = 4 * wave + rr;
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
-                        const uint32_t w = *reinterpret_cast<const uint32_t*>(&L.win[c][row][wo + 4 * j]);
+                        const uint32_t w = *reinterpret_cast<const uint32_t*>(&L.win[c][row][pos]);
                         acc[rr][c][0] = sdot4(w, tp.x, acc[rr][c][0]);
                         acc[rr][c][1] = sdot4(w, tp.y, acc[rr][c][1]);
                         acc[rr][c][2] = sdot4(w, tp.z, acc[rr][c][2]);
@@ -335,7 +257,7 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
             for (int j = 0; j < ngs; ++j) {
                 const uint4 cur = tp;
                 if (j + 1 < ngs) tp = tpg[(int64_t)(j + 1) * h.out_len];  // prefetch next group
-                step(j, cur);
+                step((hd.x + 4 * j) & (RING - 1), cur);
             }
             uint32_t outc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -435,7 +357,8 @@ k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, u
 template <int NR, bool ZONES, int CN>
 void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                   const ipp_pipe_desc* descs, int tx, int ty, const ipp_hsv_params& hp) {
-    hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, tx, ty, hp);
+    (void)tx;
+    hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
 }
 
 template <int NR>
@@ -466,8 +389,8 @@ extern "C" int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* c
     if (n_images == 0) return IPP_OK;
     if (!src || !tmp || !coefs || !descs || !hsv || n_images < 0 || max_out_w <= 0 || max_rows <= 0) return IPP_E_ARG;
     if (src_cn != 3 && src_cn != 4) return IPP_E_ARG;
-    const int tx = (max_out_w + HX - 1) / HX, ty = (max_rows + HR - 1) / HR;
-    const int64_t blocks = (int64_t)tx * ty * n_images;
+    const int tx = 1, ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
+    const int64_t blocks = (int64_t)ty * n_images;
     if (blocks >= INT32_MAX) return IPP_E_ARG;
     const dim3 grid((uint32_t)blocks);
     hipStream_t s = (hipStream_t)stream;
@@ -512,11 +435,11 @@ extern "C" int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* d
     const int ty = (bg_h + VR - 1) / VR;
     const int64_t blocks = (int64_t)ty * n_images;
     if (blocks >= INT32_MAX) return IPP_E_ARG;
-    // Composite store policy (IPP_VB_STORE = 0 plain, 1 sc1, 2 nt; default sc1:
+    // Composite store policy (IPP_VB_STORE = 0 plain, 1 sc1, 2 nt; default nt:
     // the write-once output then does not evict the shared backgrounds).
     static const int policy = [] {
         const char* e = getenv("IPP_VB_STORE");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 2;
     }();
     const dim3 grid((uint32_t)blocks);
     hipStream_t s = (hipStream_t)stream;

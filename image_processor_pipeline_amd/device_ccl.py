@@ -3,8 +3,9 @@
 Reference: transforms/pixels_isolés.py:29-61 (threshold α > 1, 8-connected
 components, keep the largest — lowest label on ties —, α := 0 elsewhere) and
 :74-81 (crop to the bbox of α ≠ 0; cv2.boundingRect(None) raises when no pixel
-is left).  All work runs in libipp.so (ipp_ccl_keep_largest); the host only
-reads back four ints per image for the crop window.
+is left).  All work runs in libipp.so (ipp_ccl_keep_largest: tile-local
+labelling + border merge, csrc/ipp_ccl.hip); the host reads back four ints per
+image for the crop window.
 """
 from __future__ import annotations
 
@@ -14,11 +15,35 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .device import _require_cuda, _stream, _to_dev, copy_window
+from .device import _keep, _require_cuda, _stream, _to_dev, alpha_bbox, copy_window
 
 
-def _label_slots(h: int, w: int) -> int:
-    return 4 * ((w + 1) // 2) * ((h + 1) // 2)
+class CclScratch:
+    """Per-image scratch layout (ipp_ccl_scratch_layout) for a batch of
+    (h, w) images, packed into one device byte buffer."""
+
+    def __init__(self, dims: Sequence[Tuple[int, int]], device):
+        lib = N.load()
+        n = len(dims)
+        self.works = np.zeros(n, N.CCL_WORK)
+        one = np.zeros(1, N.CCL_WORK)
+        base = 0
+        self.max_ent = 1
+        for i, (h, w) in enumerate(dims):
+            size = lib.ipp_ccl_scratch_layout(int(w), int(h), N.np_ptr(one))
+            if size < 0:
+                N.check(int(size), "ipp_ccl_scratch_layout")
+            for f in ("lab_off", "p_off", "a_off", "ent_off"):
+                self.works[i][f] = one[0][f] + base
+            self.works[i]["ent_cap"] = one[0]["ent_cap"]
+            self.max_ent = max(self.max_ent, int(one[0]["ent_cap"]))
+            base += (int(size) + 255) // 256 * 256
+        self.bytes = base
+        self.scratch = torch.empty(max(base, 256), dtype=torch.uint8, device=device)
+        self.works_dev = _to_dev(self.works, device)
+        self.counts = torch.empty(n, dtype=torch.int32, device=device)
+        self.stats = torch.empty(n, dtype=torch.int64, device=device)
+        self.bbox = torch.empty(4 * n, dtype=torch.int32, device=device)
 
 
 def keep_largest_masks(imgs: Sequence[torch.Tensor]) -> List[Optional[Tuple[int, int, int, int]]]:
@@ -29,9 +54,7 @@ def keep_largest_masks(imgs: Sequence[torch.Tensor]) -> List[Optional[Tuple[int,
     dev = imgs[0].device
     n = len(imgs)
     d = np.zeros(n, N.IMAGE_DESC)
-    lab_off = np.zeros(n, np.int64)
     off = 0
-    loff = 0
     flat = []
     for i, im in enumerate(imgs):
         _require_cuda(im, "keep_largest_component")
@@ -39,29 +62,33 @@ def keep_largest_masks(imgs: Sequence[torch.Tensor]) -> List[Optional[Tuple[int,
             raise ValueError("keep_largest_component expects (H, W, 4) images")
         h, w, _ = im.shape
         d[i]["off"], d[i]["w"], d[i]["h"], d[i]["pitch"], d[i]["cn"] = off, w, h, 4 * w, 4
-        lab_off[i] = loff
-        loff += _label_slots(h, w)
         off += h * w * 4
         flat.append(im.contiguous().reshape(-1))
     buf = torch.cat(flat) if n > 1 else flat[0]
-    labels = torch.empty(max(loff, 1), dtype=torch.int32, device=dev)
-    area = torch.empty(max(loff, 1), dtype=torch.int32, device=dev)
-    stats = torch.empty(n, dtype=torch.int64, device=dev)
-    bbox = torch.empty(4 * n, dtype=torch.int32, device=dev)
+    sc = CclScratch([(int(im.shape[0]), int(im.shape[1])) for im in imgs], dev)
     mw = max(int(im.shape[1]) for im in imgs)
     mh = max(int(im.shape[0]) for im in imgs)
-    dd, lo = _to_dev(d, dev), _to_dev(lab_off, dev)
-    N.check(N.load().ipp_ccl_keep_largest(buf.data_ptr(), dd.data_ptr(), n, mw, mh, labels.data_ptr(),
-                                          lo.data_ptr(), area.data_ptr(), stats.data_ptr(), bbox.data_ptr(),
-                                          _stream(dev)), "ipp_ccl_keep_largest")
+    dd = _to_dev(d, dev)
+    N.check(N.load().ipp_ccl_keep_largest(buf.data_ptr(), dd.data_ptr(), n, mw, mh, sc.works_dev.data_ptr(),
+                                          sc.scratch.data_ptr(), sc.max_ent, sc.counts.data_ptr(),
+                                          sc.stats.data_ptr(), sc.bbox.data_ptr(), _stream(dev)),
+            "ipp_ccl_keep_largest")
+    _keep(dd)
     off = 0
     for im in imgs:  # write back when the inputs were not contiguous views of buf
         sz = im.numel()
-        if n > 1 or not im.is_contiguous():
+        if n > 1 or not im.is_contiguous() or im.data_ptr() != buf.data_ptr():
             im.copy_(buf[off:off + sz].view(im.shape))
         off += sz
-    bb = bbox.cpu().numpy().reshape(n, 4)
-    return [None if r[0] < 0 else tuple(int(v) for v in r) for r in bb]
+    bb = sc.bbox.cpu().numpy().reshape(n, 4)
+    out: List[Optional[Tuple[int, int, int, int]]] = []
+    for i, r in enumerate(bb):
+        if r[0] >= 0:
+            out.append(tuple(int(v) for v in r))
+        else:
+            # no component: α was left unchanged (label 0 kept) — crop to its α ≠ 0 pixels
+            out.append(alpha_bbox([imgs[i]])[0])
+    return out
 
 
 def keep_largest_component(img: torch.Tensor) -> torch.Tensor:

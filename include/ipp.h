@@ -85,6 +85,15 @@ typedef struct ipp_copy_desc {
 int ipp_copy_window(const uint8_t* src, uint8_t* dst, const ipp_copy_desc* descs,
                     int32_t n_images, int32_t max_w, int32_t max_h, void* stream);
 
+/* Crop-fit with the window taken from a DEVICE bbox array (x0, y0, x1, y1 per
+ * image, as ipp_alpha_bbox / ipp_ccl_keep_largest write it) — the
+ * pixels_isolés.py:74-81 `_crop_fit` slice without a host round trip.  The
+ * descriptor's x0/y0/w/h are ignored; images whose bbox is empty (x0 < 0) are
+ * not written.  max_w/max_h bound the windows (pixels); cn = bytes per pixel. */
+int ipp_crop_to_bbox(const uint8_t* src, uint8_t* dst, const ipp_copy_desc* descs,
+                     const int32_t* bbox, int32_t n_images, int32_t max_w, int32_t max_h,
+                     int32_t cn, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* K6+K7: OpenCV BGR2HSV (8-bit) + inRange × R + zone AND + OR + NOT → alpha */
 /* filtres_liste.py:84 imread(BGR) :90 cvtColor :97-123 inRange/zone/OR/NOT  */
@@ -188,15 +197,42 @@ int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
 /* :32 threshold(α,1,255) :35 connectedComponentsWithStats(8) :38-55 keep    */
 /* largest :74-81 crop-fit (findNonZero + boundingRect).                     */
 /* ------------------------------------------------------------------------ */
-/* labels: int32 scratch, w*h per image (caller-provided, at image_desc.off/cn
- * scaled: label index base = lab_off[i]).  stats: int64 scratch of
- * 8 words per image (best key, bbox).  Output: α outside the largest
- * component zeroed IN PLACE in img; bbox[i] = (x0, y0, x1, y1) of α≠0 or
- * (-1,-1,-1,-1) when the image has no α≠0 pixel. */
+/* Scratch of one image inside a caller-provided byte buffer (offsets in
+ * bytes, 256-B aligned; ipp_ccl_scratch_layout fills them for a w×h image
+ * relative to 0 — add the image's base offset).  lab: uint16 per pixel (local
+ * root in its 64×32 tile); P/A: int32/uint32 per block-raster index (touched
+ * at component roots only); ent: ent_cap {root, area} pairs. */
+typedef struct ipp_ccl_work {
+    int64_t lab_off, p_off, a_off, ent_off;
+    int64_t ent_cap;
+} ipp_ccl_work;
+
+/* Bytes of scratch for one w×h image; fills *work (may be NULL). */
+int64_t ipp_ccl_scratch_layout(int32_t w, int32_t h, ipp_ccl_work* work);
+
+/* α > 1 → 8-connected components → α := 0 outside the largest (lowest root on
+ * ties) IN PLACE on 4-channel images; images without any component are left
+ * unchanged.  works: device array of per-image scratch offsets into `scratch`;
+ * max_ent = largest ent_cap; counts: int32[n] scratch; stats: int64[n]
+ * scratch (best key = area << 32 | ~root); bbox[i] = (x0, y0, x1, y1) of the
+ * kept component or (-1,-1,-1,-1) when there is none (the caller then takes
+ * the α ≠ 0 bbox of the unchanged image, pixels_isolés.py:74-81). */
 int ipp_ccl_keep_largest(uint8_t* img, const ipp_image_desc* descs, int32_t n_images,
-                         int32_t max_w, int32_t max_h, int32_t* labels,
-                         const int64_t* lab_off, uint32_t* area, int64_t* stats,
+                         int32_t max_w, int32_t max_h, const ipp_ccl_work* works,
+                         uint8_t* scratch, int64_t max_ent, int32_t* counts, int64_t* stats,
                          int32_t* bbox, void* stream);
+
+/* Fused config-5 chain on 3-channel BGR frames: filtres_liste's HSV mask
+ * (filtres_liste.py:84-134, params as for ipp_hsv_mask with bgr = 1) → α > 1
+ * components → keep the largest → crop-fit (pixels_isolés.py:29-81), written
+ * as BGRA (α 255 inside the component, 0 elsewhere) at out_descs[i] (the
+ * slot must hold the whole frame).  bbox as above; a frame with no kept pixel
+ * gets bbox (-1,...) and no output (the reference raises there). */
+int ipp_video_keep_largest(const uint8_t* frames, const ipp_image_desc* descs, int32_t n_images,
+                           int32_t max_w, int32_t max_h, const ipp_hsv_params* hsv,
+                           const ipp_ccl_work* works, uint8_t* scratch, int64_t max_ent,
+                           int32_t* counts, int64_t* stats, int32_t* bbox, uint8_t* out,
+                           const ipp_image_desc* out_descs, void* stream);
 
 /* Bounding box of non-zero pixels, Pillow getbbox() rule (rotations.py:99,
  * recadrages.py:70): the alpha band for 2/4-channel images, any band for

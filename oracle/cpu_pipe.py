@@ -63,13 +63,35 @@ def _item_rotflip(src, bg, rng):
     return ops.flip(np.asarray(rot), rng.sample(["o", "h", "v", "hv"], 1)[0])
 
 
+def _item_video4k(src, bg, rng):
+    """filtres_liste mask (NumPy restatement of cvtColor+inRange) then
+    pixels_isolés keep-largest + crop-fit (SciPy labelling for cv2 CCL)."""
+    return ops.keep_largest_component(ops.color_mask_bgra(src, REF_RANGES))
+
+
+def _video_frame(nrng, h=2160, w=3840):
+    f = np.empty((h, w, 3), np.uint8)
+    f[...] = (24, 18, 30)
+    yy, xx = np.mgrid[0:h, 0:w]
+    u = nrng.random(4)
+    cx, cy, ax, ay = w * (0.3 + 0.4 * u[0]), h * (0.3 + 0.4 * u[1]), w * (0.22 + 0.08 * u[2]), h * (0.22 + 0.08 * u[3])
+    f[((xx - cx) / ax) ** 2 + ((yy - cy) / ay) ** 2 <= 1.0] = (220, 140, 40)
+    sp = nrng.random((h, w)) < 0.005
+    f[sp] = nrng.integers(0, 256, (int(sp.sum()), 3), np.uint8)
+    return f
+
+
 def _worker(task):
     seed, count, size, workload = task
     nrng = np.random.default_rng(seed)
-    srcs = [nrng.integers(0, 256, (size, size, 3), np.uint8) for _ in range(count)]
-    bg = nrng.integers(0, 256, (size, size, 3), np.uint8)
+    if workload == "video4k":
+        srcs = [_video_frame(nrng) for _ in range(count)]
+        bg = None
+    else:
+        srcs = [nrng.integers(0, 256, (size, size, 3), np.uint8) for _ in range(count)]
+        bg = nrng.integers(0, 256, (size, size, 3), np.uint8)
     rng = random.Random(seed)
-    fn = _item_pipe5 if workload == "pipe5" else _item_rotflip
+    fn = {"pipe5": _item_pipe5, "rotflip": _item_rotflip, "video4k": _item_video4k}[workload]
     fn(srcs[0], bg, rng)  # warm imports / allocator
     t0 = time.perf_counter()
     for s in srcs:
@@ -93,7 +115,8 @@ def measure(sample: int = 192, size: int = 1024, workload: str = "pipe5") -> dic
         res = pool.map(_worker, tasks)
     wall = max(t for t, _ in res)
     items = sum(c for _, c in res)
-    mpix = items * size * size / 1e6
+    px = 3840 * 2160 if workload == "video4k" else size * size
+    mpix = items * px / 1e6
     per_item = sum(t for t, _ in res) / items
     model = platform.processor() or ""
     try:
@@ -109,9 +132,10 @@ def measure(sample: int = 192, size: int = 1024, workload: str = "pipe5") -> dic
         "unit": "Mpix/s",
         "cores": workers,
         "kind": "port",
-        "sample": f"{items} items of {size}x{size}x3 ({workload}), {workers} worker processes, in-memory, "
-                  f"Pillow {__import__('PIL').__version__} + NumPy (cv2 ops via the NumPy restatement)",
-        "value_1core": round(size * size / 1e6 / per_item, 2),
+        "sample": (f"{items} items of {'3840x2160' if workload == 'video4k' else f'{size}x{size}'}x3 ({workload}), "
+                   f"{workers} worker processes, in-memory, Pillow {__import__('PIL').__version__} + NumPy "
+                   f"(cv2 ops via the NumPy/SciPy restatement)"),
+        "value_1core": round(px / 1e6 / per_item, 2),
         "cpu_model": model,
     }
 

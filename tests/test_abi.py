@@ -39,6 +39,7 @@ STRUCTS = {
     "ipp_resample_desc": N.RESAMPLE_DESC,
     "ipp_paste_desc": N.PASTE_DESC,
     "ipp_pipe_desc": N.PIPE_DESC,
+    "ipp_ccl_work": N.CCL_WORK,
 }
 
 

@@ -271,3 +271,65 @@ def test_keep_largest_component_vs_oracle(D):
         got = device_ccl.keep_largest_component(_t(im)).cpu().numpy()
         exp = ops.keep_largest_component(im)
         assert np.array_equal(got, exp), im.shape
+
+
+# --------------------------------------------------------------------------- config 5: 4K video chain
+
+def test_video_chain_4k_vs_oracle(D):
+    """BASELINE config 5 at full size: HSV mask → keep-largest → crop-fit on
+    structured 3840×2160 frames, bit-exact vs the oracle; a frame with no
+    foreground yields no crop (the reference raises there)."""
+    from image_processor_pipeline_amd import geometry as G
+    from image_processor_pipeline_amd.video_chain import VideoChain, synthetic_frames
+    frames = synthetic_frames(3, 2160, 3840, 2, DEV)
+    frames[2, ..., 0], frames[2, ..., 1], frames[2, ..., 2] = 24, 18, 30      # background only
+    chain = VideoChain(3, 2160, 3840, DEV)
+    chain.run(frames)
+    res = chain.results()
+    host = frames.cpu().numpy()
+    for i in range(2):
+        exp = ops.keep_largest_component(ops.color_mask_bgra(host[i], G.REFERENCE_HSV_RANGES))
+        assert res[i] is not None and np.array_equal(res[i], exp), i
+    assert res[2] is None
+    # the staged form (mask → keep-largest → crop) gives the same crops, and
+    # its mask stage alone matches the oracle
+    chain.out.zero_()
+    chain.run_staged(frames)
+    staged = chain.results()
+    assert all(np.array_equal(a, b) for a, b in zip(staged[:2], res[:2])) and staged[2] is None
+    chain.mask(frames)
+    torch.cuda.synchronize()
+    assert np.array_equal(chain.bgra[0].cpu().numpy(), ops.color_mask_bgra(host[0], G.REFERENCE_HSV_RANGES))
+
+
+def test_crop_to_bbox_and_vector_copy(D):
+    from image_processor_pipeline_amd import _native as N
+    rng = np.random.default_rng(21)
+    for cn in (1, 3, 4):
+        img = rng.integers(0, 256, (37, 53, cn), np.uint8)
+        for win in [(0, 0, 53, 37), (5, 3, 17, 9), (1, 2, 52, 35), (50, 36, 3, 1)]:
+            for fl in (0, 1, 2, 3):
+                x0, y0, w, h = win
+                exp = img[y0:y0 + h, x0:x0 + w]
+                exp = exp[:, ::-1] if fl & 1 else exp
+                exp = exp[::-1] if fl & 2 else exp
+                got = D.copy_window(_t(img), win, flip=fl).cpu().numpy()
+                assert np.array_equal(got, exp), (cn, win, fl)
+    n, h, w = 3, 31, 45
+    imgs = rng.integers(0, 256, (n, h, w, 4), np.uint8)
+    bbox = np.array([[3, 4, 40, 30], [-1, -1, -1, -1], [0, 0, 45, 31]], np.int32)
+    cd = np.zeros(n, N.COPY_DESC)
+    for i in range(n):
+        cd[i]["src_off"] = cd[i]["dst_off"] = i * h * w * 4
+        cd[i]["src_pitch"] = cd[i]["dst_pitch"] = 4 * w
+        cd[i]["cn"] = 4
+    src = _t(imgs)
+    dst = torch.zeros_like(src)
+    bb = _t(bbox.reshape(-1))
+    cdd = D._to_dev(cd, src.device)
+    N.check(N.load().ipp_crop_to_bbox(src.data_ptr(), dst.data_ptr(), cdd.data_ptr(), bb.data_ptr(), n, w, h, 4,
+                                      D._stream(src.device)), "ipp_crop_to_bbox")
+    out = dst.cpu().numpy()
+    assert np.array_equal(out[0, :26, :37], imgs[0, 4:30, 3:40])
+    assert not out[1].any()
+    assert np.array_equal(out[2], imgs[2])

@@ -1,11 +1,10 @@
 #!/bin/bash
-# Quick GPU experiment: pipe parity subset, then the bench under each
-# IPP_VB_STORE policy.  Each GPU step has its own limit; stops at first failure.
+# GPU session: the GPU test suite, then the pipe5 and video4k benches.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -x -q -k "pipe or hsv" > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 21; }
+timeout -k 10 900 python -m pytest tests -m gpu -x -q ${TESTS:+-k "$TESTS"} > gpurun_out/t.log 2>&1 || { tail -40 gpurun_out/t.log; exit 21; }
 tail -1 gpurun_out/t.log
-for p in ${POLICIES:-1 0 2}; do
-  IPP_VB_STORE=$p timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/b_$p.log 2>&1 || { tail -20 gpurun_out/b_$p.log; exit 22; }
-  echo "policy $p: $(python -c "import json,sys; d=json.loads(open('gpurun_out/b_$p.log').read().strip().splitlines()[-1]); print(d['value'], d['kernels_ms'])")"
+for w in ${WORKLOADS:-pipe5 video4k}; do
+  timeout -k 10 400 python bench.py --no-cpu-baseline --workload $w > gpurun_out/b_$w.log 2>&1 || { tail -20 gpurun_out/b_$w.log; exit 22; }
+  python -c "import json; d=json.loads(open('gpurun_out/b_$w.log').read().strip().splitlines()[-1]); print('$w', d['value'], d['kernels_ms'], d['roofline']['frac'])"
 done
