@@ -16,22 +16,28 @@
 // is therefore "smallest root" (restated; UNPINNED: OpenCV is absent here).
 //
 // Algorithm (tile-local labelling, then border merging):
-//   K1 k_ccl_tile     one 64×32 tile per block: fg bits (α > 1, or the fused
-//                     HSV mask) → LDS union-find → per-pixel local root
-//                     (uint16, raster) + one entry per local component
-//                     {global root index, area}; P[root] = root, A[root] = 0.
-//   K2 k_ccl_border   unites the local roots of 8-adjacent fg pixel pairs that
-//                     straddle a tile border (global atomicMin union-find on
-//                     P, touched only at local roots).
+//   K1 k_ccl_tile     one 64×32 tile per block, one wave per row: fg bits
+//                     (α > 1, or the fused HSV mask) by ballot → horizontal
+//                     runs labelled without atomics (run start = highest
+//                     clear bit below the lane) → one LDS union per pair of
+//                     8-adjacent runs in consecutive rows → per-pixel local
+//                     root (uint16, raster) → per-component area and row /
+//                     column masks (bbox) by wave-aggregated LDS atomics →
+//                     one entry per local
+//                     component {global root, area, bbox}; P[root] = root.
+//   K2 k_ccl_border   unites the local roots of 8-adjacent fg pixel pairs
+//                     straddling a tile border, skipping pairs a neighbouring
+//                     border pixel already unites (global atomicMin
+//                     union-find on P, touched only at local roots).
 //   K3 k_ccl_resolve  per entry: R = find(P, L); A[R] += area; P[L] = R.
-//   K4 k_ccl_best     per entry that is a global root: atomicMax of
-//                     (area << 32 | ~root) per image.
-//   K5 k_ccl_bbox     bbox of the best component's pixels.
-//   K6 k_ccl_emit     in place: α := 0 outside the best component (plugin
-//                     path), or crop-fit into an output slot writing BGRA with
-//                     α = 255 inside the component (fused chain).
-// Every pixel is read once in K1 and once in K5/K6; P/A/entries are touched
-// per component, not per pixel.
+//   K4 k_ccl_best     per global root: atomicMax of (area << 32 | ~root).
+//   K5 k_ccl_bbox     per entry of the best component: bbox atomics.
+//   K6 k_ccl_emit     per tile meeting the output: flags of its local roots
+//                     (in the best component?) in LDS, then per pixel α := 0
+//                     outside it in place (plugin path), or the crop-fit
+//                     written as BGRA from the BGR frame (fused chain).
+// Pixels are read once in K1 and once in K6 (within the crop for the fused
+// chain); everything else is per component.
 #include <algorithm>
 
 #include "ipp_hsv.h"
@@ -140,7 +146,9 @@ struct Work {
     int32_t* P;        // 4*wb*hb parent array (touched at local roots only)
     uint32_t* A;       // 4*wb*hb areas (touched at roots only)
     int32_t* entL;     // per local component: global root index
-    uint32_t* entA;    // ... and its in-tile area
+    uint32_t* entA;    // ... its in-tile area
+    int4* entB;        // ... its bbox (x0, y0, x1, y1), image coordinates
+    int2* tile;        // per tile: (first entry, entry count)
 };
 
 __device__ __forceinline__ Work work_of(uint8_t* scratch, const ipp_ccl_work& w) {
@@ -150,7 +158,17 @@ __device__ __forceinline__ Work work_of(uint8_t* scratch, const ipp_ccl_work& w)
     k.A = reinterpret_cast<uint32_t*>(scratch + w.a_off);
     k.entL = reinterpret_cast<int32_t*>(scratch + w.ent_off);
     k.entA = reinterpret_cast<uint32_t*>(scratch + w.ent_off) + w.ent_cap;
+    k.entB = reinterpret_cast<int4*>(scratch + w.ent_off + 8 * w.ent_cap);
+    k.tile = reinterpret_cast<int2*>(scratch + w.tile_off);
     return k;
+}
+
+// Local index of the pixel with global block-raster index L inside tile (tx, ty).
+__device__ __forceinline__ int local_of(const Frame& f, int32_t L, int tx, int ty) {
+    const int32_t blk = L >> 2;
+    const int by = blk / f.wb, bx = blk - by * f.wb;
+    const int y = 2 * by + ((L >> 1) & 1), x = 2 * bx + (L & 1);
+    return lidx(x - tx * TW, y - ty * TH);
 }
 
 // Foreground source: α > 1 of a 4-channel image, or the HSV mask of a
@@ -162,8 +180,11 @@ __global__ void __launch_bounds__(256)
 k_ccl_tile(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
            const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, int32_t* __restrict__ counts,
            int tiles_per_img, int tiles_x_max, ipp_hsv_params hp) {
-    __shared__ int lab[TPX];
+    constexpr int RPW = TH / 4;  // rows per wave
+    __shared__ int lab[TPX];     // union-find parents; then per root the mask of its rows
     __shared__ uint32_t area[TPX];
+    __shared__ unsigned long long cols[TPX];  // per root: mask of its columns
+    __shared__ unsigned long long rowbits[TH];
     __shared__ int32_t sdiv[SRC == SRC_HSV ? 256 : 1], hdiv[SRC == SRC_HSV ? 256 : 1];
     __shared__ int nroots, base;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
@@ -176,19 +197,23 @@ k_ccl_tile(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ d
     const Work k = work_of(scratch, works[im]);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = tx * TW + lane;
+    const unsigned long long below = (1ull << lane) - 1ull;
 
     Ranges<SRC == SRC_HSV ? NR : 1> R;
     if (SRC == SRC_HSV) {
         sdiv[threadIdx.x] = kSdiv[threadIdx.x];
         hdiv[threadIdx.x] = kHdiv180[threadIdx.x];
         ranges_init<SRC == SRC_HSV ? NR : 1, ZONES>(R, hp, d.w, d.h);
+        __syncthreads();
     }
     if (threadIdx.x == 0) nroots = 0;
-    __syncthreads();
 
-    uint32_t fgmask = 0;  // bit k: pixel (lane, wave + 4k) is foreground
+    // A. fg bits per row (ballot) and run labels: a run's pixels point at its
+    //    first pixel, whose local index is the run minimum.
+    uint32_t fgmask = 0;
+    int startlane[RPW];
 #pragma unroll
-    for (int j = 0; j < TH / 4; ++j) {
+    for (int j = 0; j < RPW; ++j) {
         const int ly = wave + 4 * j, y = ty * TH + ly;
         bool fg = false;
         if (x < d.w && y < d.h) {
@@ -201,59 +226,102 @@ k_ccl_tile(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ d
                 fg = hsv_keep<SRC == SRC_HSV ? NR : 1, ZONES, true>(R, sdiv, hdiv, px, x, y) != 0u;
             }
         }
+        const unsigned long long bits = __ballot(fg);
+        const unsigned long long gaps = ~bits & below;
+        const int start = gaps ? 64 - __clzll(gaps) : 0;
+        startlane[j] = start;
         const int li = lidx(lane, ly);
-        lab[li] = fg ? li : -1;
+        lab[li] = fg ? lidx(start, ly) : -1;
         area[li] = 0u;
+        cols[li] = 0ull;
+        if (lane == 0) rowbits[ly] = bits;
         fgmask |= (fg ? 1u : 0u) << j;
     }
     __syncthreads();
 
-    // In-tile unions: left, up-left, up, up-right.
+    // B. one union per pair of 8-adjacent runs in rows ly-1, ly: the run start
+    //    takes the pixels above-left and above; every pixel takes the one
+    //    above-right when that pixel starts a run segment above (its left
+    //    neighbour above is background).
 #pragma unroll
-    for (int j = 0; j < TH / 4; ++j) {
-        if (!((fgmask >> j) & 1u)) continue;
-        const int ly = wave + 4 * j, li = lidx(lane, ly);
-        if (lane > 0 && lab[lidx(lane - 1, ly)] >= 0) lunite(lab, li, lidx(lane - 1, ly));
-        if (ly > 0) {
-            if (lane > 0 && lab[lidx(lane - 1, ly - 1)] >= 0) lunite(lab, li, lidx(lane - 1, ly - 1));
-            if (lab[lidx(lane, ly - 1)] >= 0) lunite(lab, li, lidx(lane, ly - 1));
-            if (lane < TW - 1 && lab[lidx(lane + 1, ly - 1)] >= 0) lunite(lab, li, lidx(lane + 1, ly - 1));
+    for (int j = 0; j < RPW; ++j) {
+        const int ly = wave + 4 * j;
+        if (ly == 0 || !((fgmask >> j) & 1u)) continue;
+        const unsigned long long up = rowbits[ly - 1];
+        const int li = lidx(lane, ly);
+        const bool at_start = lane == 0 || !((rowbits[ly] >> (lane - 1)) & 1ull);
+        const bool u = (up >> lane) & 1ull;
+        if (at_start) {
+            if (lane > 0 && ((up >> (lane - 1)) & 1ull)) lunite(lab, li, lidx(lane - 1, ly - 1));
+            if (u) lunite(lab, li, lidx(lane, ly - 1));
         }
+        if (lane < TW - 1 && ((up >> (lane + 1)) & 1ull) && !u) lunite(lab, li, lidx(lane + 1, ly - 1));
     }
     __syncthreads();
 
-    // Local roots per pixel → lab16 (raster, coalesced 2-B stores); areas.
+    // C. local root of every pixel (register), root flags: only run starts
+    //    walk the forest; the rest of a run takes its start's root by shuffle.
+    int root[RPW];
+    uint32_t rootmask = 0;
 #pragma unroll
-    for (int j = 0; j < TH / 4; ++j) {
+    for (int j = 0; j < RPW; ++j) {
+        const int li = lidx(lane, wave + 4 * j);
+        const bool fg = (fgmask >> j) & 1u;
+        const int rs = (fg && startlane[j] == lane) ? lfind(lab, li) : 0;
+        const int rr = __shfl(rs, startlane[j]);
+        root[j] = fg ? rr : -1;
+        rootmask |= (root[j] == li ? 1u : 0u) << j;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) lab[lidx(lane, wave + 4 * j)] = 0;  // now: row masks
+    __syncthreads();
+
+    // D. per row, per distinct root in the wave: area and bbox (one set of LDS
+    //    atomics per root, by the lowest lane holding it); lab16 out.
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
         const int ly = wave + 4 * j, y = ty * TH + ly;
         const bool fg = (fgmask >> j) & 1u;
-        int r = -1;
-        if (fg) {
-            r = lfind(lab, lidx(lane, ly));
-            atomicAdd(&area[r], 1u);
+        unsigned long long pending = __ballot(fg);
+        while (pending) {
+            const int leader = __ffsll((long long)pending) - 1;
+            const int r = __shfl(root[j], leader);
+            const unsigned long long same = __ballot(root[j] == r) & pending;
+            if (lane == leader) {
+                atomicAdd(&area[r], (uint32_t)__popcll(same));
+                atomicOr(&cols[r], same);
+                atomicOr(reinterpret_cast<unsigned int*>(&lab[r]), 1u << ly);
+            }
+            pending &= ~same;
         }
-        if (x < d.w && y < d.h) k.lab16[(int64_t)y * d.w + x] = fg ? (uint16_t)r : NOFG;
+        if (x < d.w && y < d.h) k.lab16[(int64_t)y * d.w + x] = fg ? (uint16_t)root[j] : NOFG;
     }
     __syncthreads();
 
-    // One entry per local component (its root is the pixel with lab == itself).
-    int slot[TH / 4];
+    // E. one entry per local component
+    int slot[RPW];
 #pragma unroll
-    for (int j = 0; j < TH / 4; ++j) {
-        slot[j] = -1;
-        const int li = lidx(lane, wave + 4 * j);
-        if (((fgmask >> j) & 1u) && lab[li] == li) slot[j] = atomicAdd(&nroots, 1);
+    for (int j = 0; j < RPW; ++j) slot[j] = ((rootmask >> j) & 1u) ? atomicAdd(&nroots, 1) : -1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        base = nroots > 0 ? atomicAdd(&counts[im], nroots) : 0;
+        k.tile[ty * f.tiles_x + tx] = make_int2(base, nroots);
     }
     __syncthreads();
-    if (threadIdx.x == 0 && nroots > 0) base = atomicAdd(&counts[im], nroots);
-    __syncthreads();
+    const int x0 = tx * TW, y0 = ty * TH;
 #pragma unroll
-    for (int j = 0; j < TH / 4; ++j) {
+    for (int j = 0; j < RPW; ++j) {
         if (slot[j] < 0) continue;
         const int ly = wave + 4 * j, li = lidx(lane, ly);
-        const int32_t L = gidx(f, x, ty * TH + ly);
-        k.entL[base + slot[j]] = L;
-        k.entA[base + slot[j]] = area[li];
+        const int32_t L = gidx(f, x, y0 + ly);
+        const int e = base + slot[j];
+        k.entL[e] = L;
+        k.entA[e] = area[li];
+        const unsigned long long cm = cols[li];
+        const uint32_t rm = (uint32_t)lab[li];
+        k.entB[e] = make_int4(x0 + __ffsll((long long)cm) - 1, y0 + __ffs((int)rm) - 1, x0 + 64 - __clzll(cm),
+                              y0 + 32 - __clz((int)rm));
         k.P[L] = L;
         k.A[L] = 0u;
     }
@@ -266,9 +334,12 @@ __device__ __forceinline__ int32_t root_of(const Frame& f, const Work& k, int x,
     return root_gidx(f, x / TW, y / TH, r);
 }
 
-// Border pairs: thread i < vert handles left pixel (64*bx - 1, y) of a
-// vertical tile border against (64*bx, y-1..y+1); the rest handle the upper
-// pixel (x, 32*by - 1) of a horizontal border against (x-1..x+1, 32*by).
+// Border pairs.  Thread i < vert owns left pixel (64*bx - 1, y) of a vertical
+// tile border and its 8-neighbours (64*bx, y-1..y+1); the rest own the upper
+// pixel (x, 32*by - 1) of a horizontal border and (x-1..x+1, 32*by).  Along a
+// border, consecutive owners usually see the same pair of roots: a pair is
+// skipped when the previous (next) owner with the same near-side root takes
+// it, so a long shared boundary costs one union, not one per pixel.
 __global__ void __launch_bounds__(256)
 k_ccl_border(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
              uint8_t* __restrict__ scratch, int chunks) {
@@ -280,58 +351,69 @@ k_ccl_border(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __res
     const Work k = work_of(scratch, works[im]);
     const int64_t vert = (int64_t)(f.tiles_x - 1) * f.h;
     const int64_t horz = (int64_t)(f.tiles_y - 1) * f.w;
+    // near side pixel (nx, ny) moving along the border by (sx, sy); far side at +(fx, fy)
+    int nx, ny, sx, sy, fx, fy, pos, len;
     if (i < vert) {
-        const int bx = 1 + (int)(i / f.h), y = (int)(i % f.h);
-        const int xl = bx * TW - 1;
-        const int32_t a = root_of(f, k, xl, y);
-        if (a < 0) return;
-        for (int dy = -1; dy <= 1; ++dy) {
-            const int yy = y + dy;
-            if (yy < 0 || yy >= f.h) continue;
-            const int32_t c = root_of(f, k, xl + 1, yy);
-            if (c >= 0) gunite(k.P, a, c);
-        }
+        const int bx = 1 + (int)(i / f.h);
+        pos = (int)(i % f.h);
+        len = f.h;
+        nx = bx * TW - 1, ny = pos, sx = 0, sy = 1, fx = 1, fy = 0;
     } else if (i < vert + horz) {
         const int64_t j = i - vert;
-        const int by = 1 + (int)(j / f.w), x = (int)(j % f.w);
-        const int yu = by * TH - 1;
-        const int32_t a = root_of(f, k, x, yu);
-        if (a < 0) return;
-        for (int dx = -1; dx <= 1; ++dx) {
-            const int xx = x + dx;
-            if (xx < 0 || xx >= f.w) continue;
-            const int32_t c = root_of(f, k, xx, yu + 1);
-            if (c >= 0) gunite(k.P, a, c);
-        }
+        const int by = 1 + (int)(j / f.w);
+        pos = (int)(j % f.w);
+        len = f.w;
+        nx = pos, ny = by * TH - 1, sx = 1, sy = 0, fx = 0, fy = 1;
+    } else {
+        return;
+    }
+    const int32_t a = root_of(f, k, nx, ny);
+    if (a < 0) return;
+    auto near_at = [&](int p) { return (p < 0 || p >= len) ? -1 : root_of(f, k, nx + (p - pos) * sx, ny + (p - pos) * sy); };
+    auto far_at = [&](int p) {
+        return (p < 0 || p >= len) ? -1 : root_of(f, k, nx + fx + (p - pos) * sx, ny + fy + (p - pos) * sy);
+    };
+    const int32_t ap = near_at(pos - 1), an = near_at(pos + 1);
+    const int32_t cp = far_at(pos - 1), c0 = far_at(pos), cn = far_at(pos + 1);
+    if (cp >= 0 && ap != a) gunite(k.P, a, cp);
+    if (c0 >= 0 && !(ap == a && cp == c0)) gunite(k.P, a, c0);
+    if (cn >= 0 && an != a) gunite(k.P, a, cn);
+}
+
+// Entry kernels run ENT_BLOCKS blocks per image striding over the image's
+// entry count (known only on the device).
+constexpr int ENT_BLOCKS = 32;
+
+__global__ void __launch_bounds__(256)
+k_ccl_resolve(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch,
+              const int32_t* __restrict__ counts) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / ENT_BLOCKS;
+    const int n = counts[im];
+    const Work k = work_of(scratch, works[im]);
+    for (int e = (int)(b - (uint32_t)im * ENT_BLOCKS) * 256 + threadIdx.x; e < n; e += ENT_BLOCKS * 256) {
+        const int32_t L = k.entL[e];
+        const int32_t R = gfind(k.P, L);
+        atomicAdd(k.A + R, k.entA[e]);
+        if (R != L) __hip_atomic_store(k.P + L, R, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 __global__ void __launch_bounds__(256)
-k_ccl_resolve(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch,
-              const int32_t* __restrict__ counts, int chunks) {
-    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / chunks;
-    const int e = (int)(b - (uint32_t)im * chunks) * 256 + threadIdx.x;
-    if (e >= counts[im]) return;
-    const Work k = work_of(scratch, works[im]);
-    const int32_t L = k.entL[e];
-    const int32_t R = gfind(k.P, L);
-    atomicAdd(k.A + R, k.entA[e]);
-    if (R != L) __hip_atomic_store(k.P + L, R, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ void __launch_bounds__(256)
 k_ccl_best(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, const int32_t* __restrict__ counts,
-           unsigned long long* __restrict__ best, int chunks) {
+           unsigned long long* __restrict__ best) {
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / chunks;
-    const int e = (int)(b - (uint32_t)im * chunks) * 256 + threadIdx.x;
+    const int im = b / ENT_BLOCKS;
+    const int n = counts[im];
+    const Work k = work_of(scratch, works[im]);
     unsigned long long key = 0ull;
-    if (e < counts[im]) {
-        const Work k = work_of(scratch, works[im]);
+    for (int e = (int)(b - (uint32_t)im * ENT_BLOCKS) * 256 + threadIdx.x; e < n; e += ENT_BLOCKS * 256) {
         const int32_t L = k.entL[e];
-        if (k.P[L] == L)
-            key = ((unsigned long long)k.A[L] << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)L);
+        if (k.P[L] == L) {
+            const unsigned long long kk =
+                ((unsigned long long)k.A[L] << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)L);
+            key = kk > key ? kk : key;
+        }
     }
     for (int off = 32; off > 0; off >>= 1) {
         const unsigned long long o = __shfl_xor(key, off);
@@ -344,50 +426,53 @@ __device__ __forceinline__ int32_t best_root(unsigned long long key) {
     return key ? (int32_t)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull)) : -1;
 }
 
-// bbox of the best component: rows of 64-pixel segments, wave min/max, then
-// four device atomics per wave.
+// K5: bbox of the best component = union of its entries' tile bboxes.
 __global__ void __launch_bounds__(256)
-k_ccl_bbox(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
-           uint8_t* __restrict__ scratch, const unsigned long long* __restrict__ best, int32_t* __restrict__ bbox,
-           int tiles_per_img, int tiles_x_max) {
+k_ccl_bbox(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, const int32_t* __restrict__ counts,
+           const unsigned long long* __restrict__ best, int32_t* __restrict__ bbox) {
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / tiles_per_img;
-    const int t = b - im * tiles_per_img;
-    const int ty = t / tiles_x_max, tx = t - ty * tiles_x_max;
-    const ipp_image_desc d = descs[im];
-    const Frame f = frame_of(d);
-    if (tx >= f.tiles_x || ty >= f.tiles_y) return;
+    const int im = b / ENT_BLOCKS;
     const int32_t broot = best_root(best[im]);
-    if (broot < 0) return;
-    const Work k = work_of(scratch, works[im]);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = tx * TW + lane;
-    int xmin = INT32_MAX, ymin = INT32_MAX, xmax = -1, ymax = -1;
-    if (x < d.w) {
-        for (int j = 0; j < TH / 4; ++j) {
-            const int y = ty * TH + wave + 4 * j;
-            if (y >= d.h) break;
-            const int32_t r = root_of(f, k, x, y);
-            if (r >= 0 && k.P[r] == broot) {
-                xmin = min(xmin, x);
-                xmax = max(xmax, x);
-                ymin = min(ymin, y);
-                ymax = max(ymax, y);
+    int4 bb = make_int4(INT32_MAX, INT32_MAX, -1, -1);
+    if (broot >= 0) {
+        const int n = counts[im];
+        const Work k = work_of(scratch, works[im]);
+        for (int e = (int)(b - (uint32_t)im * ENT_BLOCKS) * 256 + threadIdx.x; e < n; e += ENT_BLOCKS * 256) {
+            if (k.P[k.entL[e]] == broot) {
+                const int4 q = k.entB[e];
+                bb = make_int4(min(bb.x, q.x), min(bb.y, q.y), max(bb.z, q.z), max(bb.w, q.w));
             }
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
-        xmin = min(xmin, __shfl_xor(xmin, off));
-        ymin = min(ymin, __shfl_xor(ymin, off));
-        xmax = max(xmax, __shfl_xor(xmax, off));
-        ymax = max(ymax, __shfl_xor(ymax, off));
+        bb.x = min(bb.x, __shfl_xor(bb.x, off));
+        bb.y = min(bb.y, __shfl_xor(bb.y, off));
+        bb.z = max(bb.z, __shfl_xor(bb.z, off));
+        bb.w = max(bb.w, __shfl_xor(bb.w, off));
     }
-    if (lane == 0 && xmax >= 0) {
-        atomicMin(&bbox[4 * im + 0], xmin);
-        atomicMin(&bbox[4 * im + 1], ymin);
-        atomicMax(&bbox[4 * im + 2], xmax + 1);
-        atomicMax(&bbox[4 * im + 3], ymax + 1);
+    if ((threadIdx.x & 63) == 0 && bb.z >= 0) {
+        atomicMin(&bbox[4 * im + 0], bb.x);
+        atomicMin(&bbox[4 * im + 1], bb.y);
+        atomicMax(&bbox[4 * im + 2], bb.z);
+        atomicMax(&bbox[4 * im + 3], bb.w);
     }
+}
+
+// Flags (LDS) of a tile's local roots: in the best component?  Returns false
+// when the tile has no pixel of it.
+__device__ __forceinline__ bool tile_flags(const Frame& f, const Work& k, int tx, int ty, int32_t broot,
+                                           uint8_t* flag, int* any) {
+    const int2 te = k.tile[ty * f.tiles_x + tx];
+    if (threadIdx.x == 0) *any = 0;
+    __syncthreads();
+    for (int e = threadIdx.x; e < te.y; e += 256) {
+        const int32_t L = k.entL[te.x + e];
+        const bool in = k.P[L] == broot;
+        flag[local_of(f, L, tx, ty)] = in ? 1 : 0;
+        if (in) *any = 1;
+    }
+    __syncthreads();
+    return *any != 0;
 }
 
 // K6, plugin path: in place on a 4-channel image, α := 0 outside the best
@@ -396,6 +481,8 @@ __global__ void __launch_bounds__(256)
 k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
             uint8_t* __restrict__ scratch, const unsigned long long* __restrict__ best, int tiles_per_img,
             int tiles_x_max) {
+    __shared__ uint8_t flag[TPX];
+    __shared__ int any;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int im = b / tiles_per_img;
     const int t = b - im * tiles_per_img;
@@ -406,14 +493,15 @@ k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
     const int32_t broot = best_root(best[im]);
     if (broot < 0) return;
     const Work k = work_of(scratch, works[im]);
+    tile_flags(f, k, tx, ty, broot, flag, &any);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = tx * TW + lane;
     if (x >= d.w) return;
     for (int j = 0; j < TH / 4; ++j) {
         const int y = ty * TH + wave + 4 * j;
         if (y >= d.h) break;
-        const int32_t r = root_of(f, k, x, y);
-        if (r < 0 || k.P[r] != broot) {
+        const uint16_t r = k.lab16[(int64_t)y * d.w + x];
+        if (r == NOFG || !flag[r]) {
             uint8_t* a = img + d.off + (int64_t)y * d.pitch + 4 * (int64_t)x + 3;
             if (*a) *a = 0;
         }
@@ -422,34 +510,43 @@ k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
 
 // K6, fused chain: crop-fit of the BGR frame to the best component's bbox,
 // written as BGRA (α = 255 inside the component, 0 elsewhere) into the image's
-// output slot.  Each thread owns one output pixel of a 64×4 block tile.
+// output slot; one block per labelling tile that meets the bbox.
 __global__ void __launch_bounds__(256)
 k_ccl_crop_bgr(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
                const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch,
                const unsigned long long* __restrict__ best, const int32_t* __restrict__ bbox,
-               uint8_t* __restrict__ out, const ipp_image_desc* __restrict__ out_descs, int tiles_x, int tiles_y) {
+               uint8_t* __restrict__ out, const ipp_image_desc* __restrict__ out_descs, int tiles_per_img,
+               int tiles_x_max) {
+    __shared__ uint8_t flag[TPX];
+    __shared__ int any;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int per_img = tiles_x * tiles_y;
-    const int im = b / per_img;
-    const int t = b - im * per_img;
-    const int ty = t / tiles_x, tx = t - ty * tiles_x;
+    const int im = b / tiles_per_img;
+    const int t = b - im * tiles_per_img;
+    const int ty = t / tiles_x_max, tx = t - ty * tiles_x_max;
+    const ipp_image_desc d = descs[im];
+    const Frame f = frame_of(d);
+    if (tx >= f.tiles_x || ty >= f.tiles_y) return;
     const int32_t broot = best_root(best[im]);
     if (broot < 0) return;
-    const int x0 = bbox[4 * im + 0], y0 = bbox[4 * im + 1];
-    const int cw = bbox[4 * im + 2] - x0, chh = bbox[4 * im + 3] - y0;
-    const int ox = tx * 64 + (int)(threadIdx.x & 63), oy = ty * 4 + (int)(threadIdx.x >> 6);
-    if (ox >= cw || oy >= chh) return;
-    const ipp_image_desc d = descs[im];
-    const ipp_image_desc od = out_descs[im];
-    const Frame f = frame_of(d);
+    const int bx0 = bbox[4 * im + 0], by0 = bbox[4 * im + 1], bx1 = bbox[4 * im + 2], by1 = bbox[4 * im + 3];
+    if (tx * TW >= bx1 || (tx + 1) * TW <= bx0 || ty * TH >= by1 || (ty + 1) * TH <= by0) return;
     const Work k = work_of(scratch, works[im]);
-    const int x = x0 + ox, y = y0 + oy;
-    const bool wide_ok = (y < d.h - 1) || (x < d.w - 1);
-    const uint32_t px = load_rgb_opaque(img + d.off + (int64_t)y * d.pitch + 3 * (int64_t)x, wide_ok);
-    const int32_t r = root_of(f, k, x, y);
-    const bool in = r >= 0 && k.P[r] == broot;
-    reinterpret_cast<uint32_t*>(out + od.off + (int64_t)oy * od.pitch)[ox] =
-        (px & 0x00FFFFFFu) | (in ? 0xFF000000u : 0u);
+    tile_flags(f, k, tx, ty, broot, flag, &any);
+    const ipp_image_desc od = out_descs[im];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = tx * TW + lane;
+    if (x < bx0 || x >= bx1) return;
+    for (int j = 0; j < TH / 4; ++j) {
+        const int y = ty * TH + wave + 4 * j;
+        if (y < by0) continue;
+        if (y >= by1) break;
+        const bool wide_ok = (y < d.h - 1) || (x < d.w - 1);
+        const uint32_t px = load_rgb_opaque(img + d.off + (int64_t)y * d.pitch + 3 * (int64_t)x, wide_ok);
+        const uint16_t r = k.lab16[(int64_t)y * d.w + x];
+        const bool in = r != NOFG && flag[r];
+        reinterpret_cast<uint32_t*>(out + od.off + (int64_t)(y - by0) * od.pitch)[x - bx0] =
+            (px & 0x00FFFFFFu) | (in ? 0xFF000000u : 0u);
+    }
 }
 
 __global__ void k_ccl_prep(int32_t* bbox, unsigned long long* best, int32_t* counts, int n) {
@@ -483,7 +580,8 @@ Launch plan_launch(int n, int max_w, int max_h, int64_t max_ent) {
     L.tiles_per_img = L.tiles_x * L.tiles_y;
     const int64_t border = (int64_t)(L.tiles_x - 1) * max_h + (int64_t)(L.tiles_y - 1) * max_w;
     L.border_chunks = (int)std::max<int64_t>(1, (border + 255) / 256);
-    L.ent_chunks = (int)std::max<int64_t>(1, (max_ent + 255) / 256);
+    (void)max_ent;
+    L.ent_chunks = ENT_BLOCKS;
     const int64_t tb = (int64_t)L.tiles_per_img * n, bb = (int64_t)L.border_chunks * n, eb = (int64_t)L.ent_chunks * n;
     L.ok = tb < INT32_MAX && bb < INT32_MAX && eb < INT32_MAX;
     L.tile_grid = dim3((uint32_t)tb);
@@ -519,10 +617,9 @@ int run_labels(int src, const uint8_t* img, const ipp_image_desc* descs, int32_t
         else launch_tiles<SRC_HSV, IPP_MAX_HSV_RANGES, true>(L, s, img, descs, works, scratch, counts, q);
     }
     hipLaunchKernelGGL(k_ccl_border, L.border_grid, dim3(256), 0, s, descs, works, scratch, L.border_chunks);
-    hipLaunchKernelGGL(k_ccl_resolve, L.ent_grid, dim3(256), 0, s, works, scratch, counts, L.ent_chunks);
-    hipLaunchKernelGGL(k_ccl_best, L.ent_grid, dim3(256), 0, s, works, scratch, counts, best, L.ent_chunks);
-    hipLaunchKernelGGL(k_ccl_bbox, L.tile_grid, dim3(256), 0, s, descs, works, scratch, best, bbox, L.tiles_per_img,
-                       L.tiles_x);
+    hipLaunchKernelGGL(k_ccl_resolve, L.ent_grid, dim3(256), 0, s, works, scratch, counts);
+    hipLaunchKernelGGL(k_ccl_best, L.ent_grid, dim3(256), 0, s, works, scratch, counts, best);
+    hipLaunchKernelGGL(k_ccl_bbox, L.ent_grid, dim3(256), 0, s, works, scratch, counts, best, bbox);
     return IPP_OK;
 }
 
@@ -543,7 +640,8 @@ extern "C" int64_t ipp_ccl_scratch_layout(int32_t w, int32_t h, ipp_ccl_work* wo
     k.a_off = k.p_off + al(4 * slots);
     k.ent_off = k.a_off + al(4 * slots);
     k.ent_cap = cap;
-    const int64_t total = k.ent_off + al(8 * cap);
+    k.tile_off = k.ent_off + al(24 * cap);
+    const int64_t total = k.tile_off + al(8 * tiles);
     if (work) *work = k;
     return total;
 }
@@ -584,11 +682,8 @@ extern "C" int ipp_video_keep_largest(const uint8_t* frames, const ipp_image_des
     const int rc = run_labels(SRC_HSV, frames, descs, n_images, max_w, max_h, hsv, works, scratch, max_ent, counts,
                               best, bbox, s, L);
     if (rc != IPP_OK) return rc;
-    const int tx = (max_w + 63) / 64, ty = (max_h + 3) / 4;
-    const int64_t blocks = (int64_t)tx * ty * n_images;
-    if (blocks >= INT32_MAX) return IPP_E_ARG;
-    hipLaunchKernelGGL(k_ccl_crop_bgr, dim3((uint32_t)blocks), dim3(256), 0, s, frames, descs, works, scratch, best,
-                       bbox, out, out_descs, tx, ty);
+    hipLaunchKernelGGL(k_ccl_crop_bgr, L.tile_grid, dim3(256), 0, s, frames, descs, works, scratch, best, bbox, out,
+                       out_descs, L.tiles_per_img, L.tiles_x);
     hipLaunchKernelGGL(k_ccl_finish, dim3((n_images + 255) / 256), dim3(256), 0, s, bbox, n_images);
     IPP_CHECK_LAUNCH();
     return IPP_OK;

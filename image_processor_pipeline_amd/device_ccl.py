@@ -33,7 +33,7 @@ class CclScratch:
             size = lib.ipp_ccl_scratch_layout(int(w), int(h), N.np_ptr(one))
             if size < 0:
                 N.check(int(size), "ipp_ccl_scratch_layout")
-            for f in ("lab_off", "p_off", "a_off", "ent_off"):
+            for f in ("lab_off", "p_off", "a_off", "ent_off", "tile_off"):
                 self.works[i][f] = one[0][f] + base
             self.works[i]["ent_cap"] = one[0]["ent_cap"]
             self.max_ent = max(self.max_ent, int(one[0]["ent_cap"]))
