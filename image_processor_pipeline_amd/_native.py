@@ -22,6 +22,8 @@ IPP_E_ARG = -1
 IPP_E_LAUNCH = -2
 IPP_E_RANGE = -3
 IPP_MAX_HSV_RANGES = 16
+IPP_TAPS_DOT4 = 0
+IPP_TAPS_MFMA = 1
 IPP_RS_PREMULTIPLY = 1
 IPP_RS_UNPREMULTIPLY = 2
 
@@ -85,7 +87,7 @@ SIGNATURES = {
     "ipp_lanczos_h": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ipp_lanczos_v": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ipp_paste_blend": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
-    "ipp_pipe_hpass": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "ipp_pipe_hpass": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P]),
     "ipp_pipe_vblend": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
     "ipp_ccl_keep_largest": (_I, [_P, _P, _I, _I, _I, _P, _P, _L, _P, _P, _P, _P]),
     "ipp_ccl_scratch_layout": (_L, [_I, _I, _P]),
@@ -98,6 +100,8 @@ SIGNATURES = {
     "ipp_plan_dot4_stride": (_I, [_I]),
     "ipp_plan_dot4_size": (_L, [_I, _I]),
     "ipp_plan_dot4_from_taps": (_I, [_I, _I, _P, _I, _I, _P]),
+    "ipp_plan_mfma_size": (_L, [_I, _I, _I]),
+    "ipp_plan_mfma_from_taps": (_I, [_I, _I, _I, _P, _P]),
     "ipp_plan_pipe_axes": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I]),
     "ipp_version": (ctypes.c_char_p, []),
 }

@@ -249,6 +249,81 @@ extern "C" int ipp_plan_dot4_from_taps(int32_t out_size, int32_t ksize, const in
     return IPP_OK;
 }
 
+// ---------------------------------------------------------------------------
+// MFMA tile format (H pass of the fused pipe, v_mfma_i32_16x16x64_i8).  Outputs
+// are grouped in tiles of 16; for tile t:
+//   hdr[t]  = (K0, nK, boff, 0)   K0 = first input column of the tile rounded
+//                                 down to 16, nK = 64-column K steps, boff =
+//                                 uint4 index of the tile's B blocks
+//   bias[o] = 2^21 + 128·Σk (per output; 0 for padding outputs of the last tile)
+//   B block (s, p), s < nK, p < 3: 64 lanes × 16 B; lane l holds bytes
+//           j = 0..15 of B[k = 16(l>>4) + j][col = l&15] = balanced byte p of
+//           the tap of output 16t+col at input K0 + 64s + k (0 outside support)
+// so that with pixels stored XOR 0x80 the i8 MFMA accumulators give
+//   2^21 + Σ p·k = bias + Σ_p 2^(8p) acc_p   exactly (as the dot4 format).
+// Layout per axis (int32 units): hdr[4T], bias[16T], blocks (4 int32 each).
+// ---------------------------------------------------------------------------
+namespace {
+inline int mfma_nk_bound(int32_t in_size, int32_t out_size, int32_t ksize) {
+    const double scale = (double)in_size / (double)out_size;
+    return (int)((16 + (int64_t)ceil(15.0 * scale) + 2 + ksize + 63) / 64);
+}
+}  // namespace
+
+extern "C" int64_t ipp_plan_mfma_size(int32_t in_size, int32_t out_size, int32_t ksize) {
+    if (in_size <= 0 || out_size <= 0 || ksize <= 0) return IPP_E_ARG;
+    const int64_t T = (out_size + 15) / 16;
+    return 20 * T + T * mfma_nk_bound(in_size, out_size, ksize) * 3 * 64 * 4;
+}
+
+extern "C" int ipp_plan_mfma_from_taps(int32_t in_size, int32_t out_size, int32_t ksize, const int32_t* std_taps,
+                                       int32_t* out) {
+    if (in_size <= 0 || out_size <= 0 || ksize <= 0 || !std_taps || !out) return IPP_E_ARG;
+    const int T = (out_size + 15) / 16;
+    const int nkb = mfma_nk_bound(in_size, out_size, ksize);
+    const int32_t* bounds = std_taps;
+    const int32_t* kk = std_taps + 2 * (int64_t)out_size;
+    int32_t* hdr = out;
+    int32_t* bias = out + 4 * (int64_t)T;
+    uint8_t* blocks = reinterpret_cast<uint8_t*>(out + 20 * (int64_t)T);
+    int64_t boff = 0;  // in uint4 units
+    for (int t = 0; t < T; ++t) {
+        const int o0 = 16 * t, o1 = std::min(o0 + 16, (int)out_size);
+        const int K0 = bounds[2 * o0] & ~15;
+        int end = K0;
+        for (int o = o0; o < o1; ++o) end = std::max(end, bounds[2 * o] + bounds[2 * o + 1]);
+        const int nK = (end - K0 + 63) / 64;
+        if (nK > nkb) return IPP_E_RANGE;
+        hdr[4 * t] = K0;
+        hdr[4 * t + 1] = nK;
+        hdr[4 * t + 2] = (int32_t)boff;
+        hdr[4 * t + 3] = 0;
+        uint8_t* tb = blocks + 16 * boff;
+        memset(tb, 0, (size_t)nK * 3 * 64 * 16);
+        for (int col = 0; col < 16; ++col) {
+            const int o = o0 + col;
+            if (o >= o1) {
+                bias[o] = 0;
+                continue;
+            }
+            const int xmin = bounds[2 * o], cnt = bounds[2 * o + 1];
+            int64_t sum = 0;
+            for (int q = 0; q < cnt; ++q) {
+                const int32_t k = kk[(int64_t)o * ksize + q];
+                sum += k;
+                int8_t b[3];
+                balanced_bytes(k, b);
+                const int rel = xmin + q - K0, s = rel / 64, kin = rel % 64;
+                const int lane = 16 * (kin / 16) + col, j = kin % 16;
+                for (int p = 0; p < 3; ++p) tb[((int64_t)(s * 3 + p) * 64 + lane) * 16 + j] = (uint8_t)b[p];
+            }
+            bias[o] = (int32_t)((1 << 21) + 128 * sum);
+        }
+        boff += (int64_t)nK * 3 * 64;
+    }
+    return IPP_OK;
+}
+
 // Plan every axis of a pipe batch in the dot4 format.  Axis i resamples
 // in_sizes[i] → out_sizes[i]; identity[i] != 0 encodes "no pass on this axis"
 // (single 2^22 tap).  For axes with shift_first[i] != 0 the Pillow bounds are
@@ -287,8 +362,10 @@ extern "C" int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int3
             const int first = tmp[0], last = tmp[2 * (o - 1)] + tmp[2 * (o - 1) + 1];
             first_last[2 * i] = first;
             first_last[2 * i + 1] = last;
-            const int e = ipp_plan_dot4_from_taps(o, ksize, tmp.data(), shift_first[i] ? first : 0, transposed[i],
-                                                  out + offsets[i]);
+            const int e = transposed[i] == 2
+                              ? ipp_plan_mfma_from_taps(in, o, ksize, tmp.data(), out + offsets[i])
+                              : ipp_plan_dot4_from_taps(o, ksize, tmp.data(), shift_first[i] ? first : 0,
+                                                        transposed[i], out + offsets[i]);
             if (e) err[t] = e;
         }
     };

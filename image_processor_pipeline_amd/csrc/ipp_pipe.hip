@@ -129,7 +129,7 @@ __device__ uint8_t g_dbg_win[4 * 16 * 400];
 __device__ int32_t g_dbg_meta[8];
 #endif
 
-struct HpassLds {
+struct __attribute__((aligned(16))) HpassLds {
     uint8_t win[4][HR][WSTRIDE];      // planar window ring, bytes p ^ 0x80
     int32_t sdiv[256], hdiv[256];     // OpenCV RGB2HSV_b division tables
 };
@@ -139,7 +139,9 @@ struct HpassLds {
 // the columns its predecessor did not (consecutive chunks' windows overlap by
 // the filter support), so every M pixel of the band is gathered and
 // HSV-tested exactly once.
-template <int NR, bool ZONES, int CN>
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+template <int NR, bool ZONES, int CN, int FMT>
 __global__ void __launch_bounds__(256)
 k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
              const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp) {
@@ -161,9 +163,13 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
     const Sampler S = make_sampler(src, g);
     const int ngs = h.ksize;  // tap-group stride of this item (dot4 format)
     const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
-    // H tap planes are stored transposed, [group j][output x'] (16 B each), so a
-    // wave's 64 lanes read one contiguous KiB per group.
+    // dot4: H tap planes are stored transposed, [group j][output x'] (16 B each),
+    // so a wave's 64 lanes read one contiguous KiB per group.
     const uint4* planes = reinterpret_cast<const uint4*>(coefs + h.coef_off + 4 * (int64_t)h.out_len);
+    // mfma: tile headers (K0, nK, boff), per-output bias, B blocks (ipp_host.cpp)
+    const int ntiles = (h.out_len + 15) >> 4;
+    const int32_t* tbias = coefs + h.coef_off + 4 * (int64_t)ntiles;
+    const uint4* tblk = reinterpret_cast<const uint4*>(coefs + h.coef_off + 20 * (int64_t)ntiles);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform → SGPR
     const int nrows = min(HR, h.lines - row0);
@@ -175,11 +181,27 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
     const uint32_t rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
 
     int filled = hdr[0].x;  // ring holds M columns [.., filled)
-    for (int s0 = 0; s0 < h.out_len;) {
-        int s1 = min(s0 + HX, h.out_len);
-        while (s1 - s0 > 1 && hdr[s1 - 1].x + 4 * ngs - hdr[s0].x > RING) s1 = s0 + (s1 - s0 + 1) / 2;
-        const int W1 = hdr[s1 - 1].x + 4 * ngs;   // window end (multiple of 4)
-        const int c0 = max(filled, hdr[s0].x);    // first column not in the ring
+    // Chunks: dot4 — up to HX outputs, one per lane; mfma — up to 4 tiles of 16
+    // outputs, one per wave.  A chunk's window must fit the ring.
+    const int nunits = FMT == 0 ? h.out_len : ntiles;
+    for (int s0 = 0; s0 < nunits;) {
+        int s1, W0, W1;
+        if (FMT == 0) {
+            s1 = min(s0 + HX, h.out_len);
+            while (s1 - s0 > 1 && hdr[s1 - 1].x + 4 * ngs - hdr[s0].x > RING) s1 = s0 + (s1 - s0 + 1) / 2;
+            W0 = hdr[s0].x;
+            W1 = hdr[s1 - 1].x + 4 * ngs;  // window end (multiple of 4)
+        } else {
+            W0 = hdr[s0].x;
+            s1 = min(s0 + 4, ntiles);
+            for (;;) {
+                W1 = W0;
+                for (int t = s0; t < s1; ++t) W1 = max(W1, hdr[t].x + 64 * hdr[t].y);
+                if (s1 - s0 == 1 || W1 - W0 <= RING) break;
+                --s1;
+            }
+        }
+        const int c0 = max(filled, W0);  // first column not in the ring
         const int ng4 = max(0, (W1 - c0) >> 2);
         filled = max(filled, W1);
 
@@ -226,51 +248,106 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
         }
         __syncthreads();
 
-        // Phase 2: output x' = s0 + lane, rows 4*wave .. 4*wave+3.
-        const int xo = s0 + lane;
-        if (xo < s1) {
-            const int4 hd = hdr[xo];
-            int32_t acc[4][4][3];
+        if (FMT == 0) {
+            // Phase 2: output x' = s0 + lane, rows 4*wave .. 4*wave+3.
+            const int xo = s0 + lane;
+            if (xo < s1) {
+                const int4 hd = hdr[xo];
+                int32_t acc[4][4][3];
+    #pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+    #pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[rr][c][0] = acc[rr][c][1] = acc[rr][c][2] = 0;
+                auto step = [&](int pos, const uint4 tp) {
+    #pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = 4 * wave + rr;
+    #pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const uint32_t w = *reinterpret_cast<const uint32_t*>(&L.win[c][row][pos]);
+                            acc[rr][c][0] = sdot4(w, tp.x, acc[rr][c][0]);
+                            acc[rr][c][1] = sdot4(w, tp.y, acc[rr][c][1]);
+                            acc[rr][c][2] = sdot4(w, tp.z, acc[rr][c][2]);
+                        }
+                    }
+                };
+                // One tap group per iteration: unrolling j lets the compiler merge
+                // the 4-byte-aligned window reads of j and j+1 into ds_read2_b64,
+                // which gfx950 replays at ~64 cycles when not 8-byte aligned.
+                const uint4* tpg = planes + xo;
+                uint4 tp = tpg[0];
+    #pragma unroll 1
+                for (int j = 0; j < ngs; ++j) {
+                    const uint4 cur = tp;
+                    if (j + 1 < ngs) tp = tpg[(int64_t)(j + 1) * h.out_len];  // prefetch next group
+                    step((hd.x + 4 * j) & (RING - 1), cur);
+                }
+                uint32_t outc[4] = {0u, 0u, 0u, 0u};
+    #pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+    #pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const int32_t ss = hd.z + acc[rr][c][0] + (acc[rr][c][1] << 8) + (acc[rr][c][2] << 16);
+                        outc[c] |= clip8(ss) << (8 * rr);
+                    }
+                const int grp = (row0 >> 2) + wave;
+                uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
+                *dst = make_uint4(outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
+                                  outc[3] ^ 0x80808080u);
+            }
+        } else {
+            // Phase 2 (mfma): wave w takes tile s0 + w; A = 16 window rows × 64
+            // columns of one channel (lane l: row l&15, bytes 16(l>>4)..+15),
+            // B = 64 columns × 16 outputs of one tap byte plane.  D lane l =
+            // output l&15, rows 4(l>>4)..+3 = exactly one 16-B T group.
+            const int t = s0 + wave;
+            if (t < s1) {
+                const int4 th = hdr[t];
+                i32x4 acc[4][3];
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr)
+                for (int c = 0; c < 4; ++c)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) acc[rr][c][0] = acc[rr][c][1] = acc[rr][c][2] = 0;
-            auto step = [&](int pos, const uint4 tp) {
+                    for (int p = 0; p < 3; ++p) acc[c][p] = i32x4{0, 0, 0, 0};
+                const uint4* bt = tblk + th.z + lane;
+                const int arow = lane & 15, akoff = 16 * (lane >> 4);
+                uint4 bn[3];
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) {
-                    const int row = 4 * wave + rr;
+                for (int p = 0; p < 3; ++p) bn[p] = bt[p * 64];
+#pragma unroll 1
+                for (int ks = 0; ks < th.y; ++ks) {
+                    i32x4 bq[3];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) bq[p] = __builtin_bit_cast(i32x4, bn[p]);
+                    if (ks + 1 < th.y) {
+#pragma unroll
+                        for (int p = 0; p < 3; ++p) bn[p] = bt[((ks + 1) * 3 + p) * 64];
+                    }
+                    const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
-                        const uint32_t w = *reinterpret_cast<const uint32_t*>(&L.win[c][row][pos]);
-                        acc[rr][c][0] = sdot4(w, tp.x, acc[rr][c][0]);
-                        acc[rr][c][1] = sdot4(w, tp.y, acc[rr][c][1]);
-                        acc[rr][c][2] = sdot4(w, tp.z, acc[rr][c][2]);
+                        const i32x4 a = *reinterpret_cast<const i32x4*>(&L.win[c][arow][pos]);
+#pragma unroll
+                        for (int p = 0; p < 3; ++p)
+                            acc[c][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[p], acc[c][p], 0, 0, 0);
                     }
                 }
-            };
-            // One tap group per iteration: unrolling j lets the compiler merge
-            // the 4-byte-aligned window reads of j and j+1 into ds_read2_b64,
-            // which gfx950 replays at ~64 cycles when not 8-byte aligned.
-            const uint4* tpg = planes + xo;
-            uint4 tp = tpg[0];
-#pragma unroll 1
-            for (int j = 0; j < ngs; ++j) {
-                const uint4 cur = tp;
-                if (j + 1 < ngs) tp = tpg[(int64_t)(j + 1) * h.out_len];  // prefetch next group
-                step((hd.x + 4 * j) & (RING - 1), cur);
-            }
-            uint32_t outc[4] = {0u, 0u, 0u, 0u};
+                const int xo = 16 * t + (lane & 15);
+                if (xo < h.out_len) {
+                    const int32_t bias = tbias[xo];
+                    uint32_t outc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr)
+                    for (int c = 0; c < 4; ++c)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int32_t ss = hd.z + acc[rr][c][0] + (acc[rr][c][1] << 8) + (acc[rr][c][2] << 16);
-                    outc[c] |= clip8(ss) << (8 * rr);
+                        for (int rr = 0; rr < 4; ++rr) {
+                            const int32_t ss = bias + acc[c][0][rr] + (acc[c][1][rr] << 8) + (acc[c][2][rr] << 16);
+                            outc[c] |= clip8(ss) << (8 * rr);
+                        }
+                    const int grp = (row0 >> 2) + (lane >> 4);
+                    uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
+                    *dst = make_uint4(outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
+                                      outc[3] ^ 0x80808080u);
                 }
-            const int grp = (row0 >> 2) + wave;
-            uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
-            *dst = make_uint4(outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
-                              outc[3] ^ 0x80808080u);
+            }
         }
         __syncthreads();
         s0 = s1;
@@ -356,20 +433,22 @@ k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, u
 
 template <int NR, bool ZONES, int CN>
 void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
-                  const ipp_pipe_desc* descs, int tx, int ty, const ipp_hsv_params& hp) {
-    (void)tx;
-    hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
+                  const ipp_pipe_desc* descs, int fmt, int ty, const ipp_hsv_params& hp) {
+    if (fmt == IPP_TAPS_MFMA)
+        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
+    else
+        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 0>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
 }
 
 template <int NR>
 void launch_hpass_nr(bool zones, int cn, dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp,
-                     const int32_t* coefs, const ipp_pipe_desc* descs, int tx, int ty, const ipp_hsv_params& hp) {
+                     const int32_t* coefs, const ipp_pipe_desc* descs, int fmt, int ty, const ipp_hsv_params& hp) {
     if (zones) {
-        if (cn == 4) launch_hpass<NR, true, 4>(grid, s, src, tmp, coefs, descs, tx, ty, hp);
-        else launch_hpass<NR, true, 3>(grid, s, src, tmp, coefs, descs, tx, ty, hp);
+        if (cn == 4) launch_hpass<NR, true, 4>(grid, s, src, tmp, coefs, descs, fmt, ty, hp);
+        else launch_hpass<NR, true, 3>(grid, s, src, tmp, coefs, descs, fmt, ty, hp);
     } else {
-        if (cn == 4) launch_hpass<NR, false, 4>(grid, s, src, tmp, coefs, descs, tx, ty, hp);
-        else launch_hpass<NR, false, 3>(grid, s, src, tmp, coefs, descs, tx, ty, hp);
+        if (cn == 4) launch_hpass<NR, false, 4>(grid, s, src, tmp, coefs, descs, fmt, ty, hp);
+        else launch_hpass<NR, false, 3>(grid, s, src, tmp, coefs, descs, fmt, ty, hp);
     }
 }
 
@@ -385,11 +464,12 @@ extern "C" int ipp_dbg_dump(void* win, void* meta) {
 
 extern "C" int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
                               int32_t n_images, int32_t max_out_w, int32_t max_rows, int32_t src_cn,
-                              const ipp_hsv_params* hsv, void* stream) {
+                              const ipp_hsv_params* hsv, int32_t tap_format, void* stream) {
     if (n_images == 0) return IPP_OK;
     if (!src || !tmp || !coefs || !descs || !hsv || n_images < 0 || max_out_w <= 0 || max_rows <= 0) return IPP_E_ARG;
     if (src_cn != 3 && src_cn != 4) return IPP_E_ARG;
-    const int tx = 1, ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
+    if (tap_format != IPP_TAPS_DOT4 && tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;
+    const int fmt = tap_format, ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
     const int64_t blocks = (int64_t)ty * n_images;
     if (blocks >= INT32_MAX) return IPP_E_ARG;
     const dim3 grid((uint32_t)blocks);
@@ -403,21 +483,21 @@ extern "C" int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* c
     // A range that never matches: lo_v = 1 > hi_v = 0 (cv::inRange's empty range).
     const ipp_hsv_range never = ipp_hsv_range{{0, 0, 1}, {180, 255, 0}, {0, 0, 0, 0}};
     switch (hsv->n_ranges) {
-        case 1: launch_hpass_nr<1>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        case 2: launch_hpass_nr<2>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        case 3: launch_hpass_nr<3>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
-        case 4: launch_hpass_nr<4>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, *hsv); break;
+        case 1: launch_hpass_nr<1>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv); break;
+        case 2: launch_hpass_nr<2>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv); break;
+        case 3: launch_hpass_nr<3>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv); break;
+        case 4: launch_hpass_nr<4>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv); break;
         case 5: case 6: {
             ipp_hsv_params q = *hsv;  // pad with never-matching ranges (lo > hi in v)
             for (int k = q.n_ranges; k < 6; ++k) q.r[k] = never;
-            launch_hpass_nr<6>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, q);
+            launch_hpass_nr<6>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, q);
             break;
         }
         default: {
             if (hsv->n_ranges > IPP_MAX_HSV_RANGES) return IPP_E_ARG;
             ipp_hsv_params q = *hsv;
             for (int k = q.n_ranges; k < IPP_MAX_HSV_RANGES; ++k) q.r[k] = never;
-            launch_hpass_nr<IPP_MAX_HSV_RANGES>(zones, cn, grid, s, src, tmp, coefs, descs, tx, ty, q);
+            launch_hpass_nr<IPP_MAX_HSV_RANGES>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, q);
             break;
         }
     }

@@ -18,6 +18,7 @@ device work is two launches for the whole batch (``ipp_pipe_hpass``,
 from __future__ import annotations
 
 import math
+import os
 import random
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
@@ -30,6 +31,8 @@ from . import geometry as G
 from .device import SYM_FLIP, _stream, _to_dev
 
 ALL_SYMS = ("o", "h", "v", "hv")
+# H-pass tap format: "mfma" (v_mfma_i32_16x16x64_i8 tiles) or "dot4" (VALU)
+TAPS = os.environ.get("IPP_TAPS", "mfma")
 
 
 @dataclass
@@ -70,6 +73,7 @@ class PipePlan:
     bg_h: int
     algo_bytes_hpass: int = 0
     algo_bytes_vblend: int = 0
+    tap_format: int = 0                   # IPP_TAPS_DOT4 / IPP_TAPS_MFMA (H pass)
 
 
 def draw_params(n: int, src_hw: Tuple[int, int], bg_hw: Tuple[int, int], n_bg: int, cfg: PipeConfig,
@@ -166,12 +170,16 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     ks = np.array([1 if ident[j] else lib.ipp_plan_lanczos_ksize(0.0, float(a_in[j]), int(a_out[j]))
                    for j in range(m)], np.int64)
     ngs = np.array([lib.ipp_plan_dot4_stride(int(k)) for k in ks], np.int64)
-    sizes = 4 * a_out.astype(np.int64) * (1 + ngs)
+    mfma = TAPS == "mfma"
+    # H axes (even j): mfma tiles or transposed dot4; V axes: row-major dot4
+    transp = np.array([(2 if mfma else 1) if j % 2 == 0 else 0 for j in range(m)], np.int32)
+    sizes = np.array([lib.ipp_plan_mfma_size(int(a_in[j]), int(a_out[j]), int(ks[j])) if transp[j] == 2
+                      else 4 * int(a_out[j]) * (1 + int(ngs[j])) for j in range(m)], np.int64)
+    sizes = (sizes + 3) // 4 * 4          # 16-B aligned axis blocks
     offs = np.zeros(m, np.int64)
     offs[1:] = np.cumsum(sizes)[:-1]
     coefs = np.zeros(int(sizes.sum()), np.int32)
     first_last = np.zeros(2 * m, np.int32)
-    transp = np.array([j % 2 == 0 for j in range(m)], np.int32)   # H planes [group][output]
     N.check(lib.ipp_plan_pipe_axes(m, N.np_ptr(a_in), N.np_ptr(a_out), N.np_ptr(ident), N.np_ptr(shift),
                                    N.np_ptr(transp), N.np_ptr(offs), N.np_ptr(coefs), N.np_ptr(first_last), 0),
             "ipp_plan_pipe_axes")
@@ -222,7 +230,7 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     d = d[order]
     hsv = G.hsv_params(cfg.hsv_ranges, cfg.zones, cfg.use_gimp_scale, bgr=False)
     return PipePlan(d, coefs, hsv, params, cut_dims, ov_dims, max(tmp_off, 256), max_out_w, max_rows, bw, bh,
-                    algo_h, algo_v)
+                    algo_h, algo_v, N.IPP_TAPS_MFMA if mfma else N.IPP_TAPS_DOT4)
 
 
 class PipeRunner:
@@ -240,7 +248,7 @@ class PipeRunner:
         p = self.plan
         N.check(self.lib.ipp_pipe_hpass(src.data_ptr(), self.tmp.data_ptr(), self.coefs.data_ptr(),
                                         self.descs.data_ptr(), len(p.descs), p.max_out_w, p.max_rows, 3,
-                                        N.np_ptr(p.hsv), _stream(self.device)), "ipp_pipe_hpass")
+                                        N.np_ptr(p.hsv), p.tap_format, _stream(self.device)), "ipp_pipe_hpass")
 
     def vblend(self, bgs: torch.Tensor, out: torch.Tensor) -> None:
         p = self.plan

@@ -183,11 +183,15 @@ typedef struct ipp_pipe_desc {
     ipp_paste_desc p;       /* paste: ov = V-pass result (never stored)        */
 } ipp_pipe_desc;
 
+/* H tap formats of ipp_pipe_hpass (ipp_plan_pipe_axes transposed = 1 / 2). */
+#define IPP_TAPS_DOT4 0   /* per-output dot4 planes, v_dot4 on the VALU       */
+#define IPP_TAPS_MFMA 1   /* 16-output tiles, v_mfma_i32_16x16x64_i8          */
+
 /* src_cn: channels of every source in the batch (3 or 4); hsv: HOST pointer. */
 int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                    const ipp_pipe_desc* descs, int32_t n_images,
                    int32_t max_out_w, int32_t max_rows, int32_t src_cn,
-                   const ipp_hsv_params* hsv, void* stream);
+                   const ipp_hsv_params* hsv, int32_t tap_format, void* stream);
 int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
                     const int32_t* coefs, const ipp_pipe_desc* descs, int32_t n_images,
                     int32_t bg_w, int32_t bg_h, void* stream);
@@ -271,6 +275,13 @@ int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int32_t* out_si
                        const int32_t* identity, const int32_t* shift_first,
                        const int32_t* transposed, const int64_t* offsets, int32_t* out,
                        int32_t* first_last, int32_t n_threads);
+/* MFMA tile format of an H axis for the fused pipe (v_mfma_i32_16x16x64_i8;
+ * see ipp_host.cpp): size bound in int32 for (in, out, ksize), and the
+ * conversion from standard Pillow taps.  ipp_plan_pipe_axes writes this
+ * format for axes with transposed[i] == 2. */
+int64_t ipp_plan_mfma_size(int32_t in_size, int32_t out_size, int32_t ksize);
+int ipp_plan_mfma_from_taps(int32_t in_size, int32_t out_size, int32_t ksize,
+                            const int32_t* std_taps, int32_t* out);
 /* ksize for (in_size, out_size) without computing taps. */
 int32_t ipp_plan_lanczos_ksize(double in0, double in1, int32_t out_size);
 

@@ -110,3 +110,44 @@ def test_overlay_size_and_hsv_params():
         G.hsv_params([(0, 0, 0, 200, 255, 255)])
     with pytest.raises(ValueError):
         G.hsv_params([])
+
+
+@pytest.mark.parametrize("io", [(1100, 230), (1268, 150), (896, 896), (40, 13), (1, 1), (300, 299), (57, 20)])
+def test_mfma_tile_format_is_exact(io):
+    """Emulate v_mfma_i32_16x16x64_i8 on the planned B blocks: for every
+    output, bias + Σ_p 2^(8p) Σ_s Σ_k (pix[K0+64s+k] ^ 0x80) · B_p[k][col]
+    == 2^21 + Σ p·k (the identity the MFMA H pass relies on)."""
+    lib = N.load()
+    i, o = io
+    k, std = G.lanczos_taps(i, o)
+    size = lib.ipp_plan_mfma_size(i, o, k)
+    out = np.zeros(size, np.int32)
+    assert lib.ipp_plan_mfma_from_taps(i, o, k, N.np_ptr(std), N.np_ptr(out)) == 0
+    T = (o + 15) // 16
+    hdr = out[:4 * T].reshape(T, 4)
+    bias = out[4 * T:20 * T]
+    blocks = out[20 * T:].view(np.uint8).view(np.int8).reshape(-1, 64, 16)
+    rng = np.random.default_rng(5)
+    pix = rng.integers(0, 256, i + 256, np.uint8)
+    sp = (pix ^ 0x80).view(np.int8).astype(np.int64)
+    for t in range(T):
+        K0, nK, boff = int(hdr[t, 0]), int(hdr[t, 1]), int(hdr[t, 2])
+        assert K0 % 16 == 0 and boff % 64 == 0
+        acc = np.zeros((3, 16), np.int64)
+        for s in range(nK):
+            for p in range(3):
+                blk = blocks[boff // 64 + s * 3 + p].astype(np.int64)  # [lane][j]
+                Bm = np.zeros((64, 16), np.int64)                     # B[k][col]
+                for lane in range(64):
+                    Bm[16 * (lane >> 4):16 * (lane >> 4) + 16, lane & 15] = blk[lane]
+                a = sp[K0 + 64 * s:K0 + 64 * s + 64]
+                a = np.pad(a, (0, 64 - len(a)))
+                acc[p] += a @ Bm
+        for col in range(16):
+            oo = 16 * t + col
+            if oo >= o:
+                continue
+            xmin, cnt = std[2 * oo], std[2 * oo + 1]
+            ref = (1 << 21) + int((pix[xmin:xmin + cnt].astype(np.int64) * std[2 * o + oo * k:2 * o + oo * k + cnt]).sum())
+            got = int(bias[oo]) + int(acc[0, col]) + (int(acc[1, col]) << 8) + (int(acc[2, col]) << 16)
+            assert got == ref, (t, col)
