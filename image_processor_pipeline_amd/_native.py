@@ -88,7 +88,7 @@ SIGNATURES = {
     "ipp_lanczos_v": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ipp_paste_blend": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     "ipp_pipe_hpass": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P]),
-    "ipp_pipe_vblend": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "ipp_pipe_vblend": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ipp_ccl_keep_largest": (_I, [_P, _P, _I, _I, _I, _P, _P, _L, _P, _P, _P, _P]),
     "ipp_ccl_scratch_layout": (_L, [_I, _I, _P]),
     "ipp_video_keep_largest": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _L, _P, _P, _P, _P, _P, _P]),
@@ -101,7 +101,8 @@ SIGNATURES = {
     "ipp_plan_dot4_size": (_L, [_I, _I]),
     "ipp_plan_dot4_from_taps": (_I, [_I, _I, _P, _I, _I, _P]),
     "ipp_plan_mfma_size": (_L, [_I, _I, _I]),
-    "ipp_plan_mfma_from_taps": (_I, [_I, _I, _I, _P, _P]),
+    "ipp_plan_mfma_from_taps": (_I, [_I, _I, _I, _P, _I, _I, _P]),
+    "ipp_plan_mfma_nk_bound": (_I, [_I, _I, _I]),
     "ipp_plan_pipe_axes": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I]),
     "ipp_version": (ctypes.c_char_p, []),
 }

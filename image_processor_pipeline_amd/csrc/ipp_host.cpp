@@ -250,15 +250,19 @@ extern "C" int ipp_plan_dot4_from_taps(int32_t out_size, int32_t ksize, const in
 }
 
 // ---------------------------------------------------------------------------
-// MFMA tile format (H pass of the fused pipe, v_mfma_i32_16x16x64_i8).  Outputs
-// are grouped in tiles of 16; for tile t:
+// MFMA tile format (fused pipe, v_mfma_i32_16x16x64_i8).  Outputs are grouped
+// in tiles of 16, tile t covering outputs [16t - phase, 16t - phase + 16) ∩
+// [0, out) (phase lets the V pass align tiles with 16-row background bands);
+// input indices are shifted by `shift` (the V pass's ybox_first).  For tile t:
 //   hdr[t]  = (K0, nK, boff, 0)   K0 = first input column of the tile rounded
 //                                 down to 16, nK = 64-column K steps, boff =
 //                                 uint4 index of the tile's B blocks
-//   bias[o] = 2^21 + 128·Σk (per output; 0 for padding outputs of the last tile)
-//   B block (s, p), s < nK, p < 3: 64 lanes × 16 B; lane l holds bytes
-//           j = 0..15 of B[k = 16(l>>4) + j][col = l&15] = balanced byte p of
-//           the tap of output 16t+col at input K0 + 64s + k (0 outside support)
+//   bias[16t + c] = 2^21 + 128·Σk of the tile's output c (0 for padding)
+//   block (s, p), s < nK, p < 3: 64 lanes × 16 B; lane l holds bytes
+//           j = 0..15 = balanced byte p of the tap of the tile's output l&15
+//           at input K0 + 64s + 16(l>>4) + j (0 outside its support).  This is
+//           the B operand B[k][col] of the H pass and, unchanged, the A
+//           operand A[row][k] of the V pass (same lane map).
 // so that with pixels stored XOR 0x80 the i8 MFMA accumulators give
 //   2^21 + Σ p·k = bias + Σ_p 2^(8p) acc_p   exactly (as the dot4 format).
 // Layout per axis (int32 units): hdr[4T], bias[16T], blocks (4 int32 each).
@@ -272,14 +276,20 @@ inline int mfma_nk_bound(int32_t in_size, int32_t out_size, int32_t ksize) {
 
 extern "C" int64_t ipp_plan_mfma_size(int32_t in_size, int32_t out_size, int32_t ksize) {
     if (in_size <= 0 || out_size <= 0 || ksize <= 0) return IPP_E_ARG;
-    const int64_t T = (out_size + 15) / 16;
+    const int64_t T = (out_size + 15) / 16 + 1;  // + 1: a phase may add a tile
     return 20 * T + T * mfma_nk_bound(in_size, out_size, ksize) * 3 * 64 * 4;
 }
 
+extern "C" int32_t ipp_plan_mfma_nk_bound(int32_t in_size, int32_t out_size, int32_t ksize) {
+    if (in_size <= 0 || out_size <= 0 || ksize <= 0) return IPP_E_ARG;
+    return mfma_nk_bound(in_size, out_size, ksize);
+}
+
 extern "C" int ipp_plan_mfma_from_taps(int32_t in_size, int32_t out_size, int32_t ksize, const int32_t* std_taps,
-                                       int32_t* out) {
-    if (in_size <= 0 || out_size <= 0 || ksize <= 0 || !std_taps || !out) return IPP_E_ARG;
-    const int T = (out_size + 15) / 16;
+                                       int32_t shift, int32_t phase, int32_t* out) {
+    if (in_size <= 0 || out_size <= 0 || ksize <= 0 || !std_taps || !out || phase < 0 || phase > 15)
+        return IPP_E_ARG;
+    const int T = (out_size + phase + 15) / 16;
     const int nkb = mfma_nk_bound(in_size, out_size, ksize);
     const int32_t* bounds = std_taps;
     const int32_t* kk = std_taps + 2 * (int64_t)out_size;
@@ -288,10 +298,11 @@ extern "C" int ipp_plan_mfma_from_taps(int32_t in_size, int32_t out_size, int32_
     uint8_t* blocks = reinterpret_cast<uint8_t*>(out + 20 * (int64_t)T);
     int64_t boff = 0;  // in uint4 units
     for (int t = 0; t < T; ++t) {
-        const int o0 = 16 * t, o1 = std::min(o0 + 16, (int)out_size);
-        const int K0 = bounds[2 * o0] & ~15;
+        const int o0 = 16 * t - phase, o1 = std::min(o0 + 16, (int)out_size), oa = std::max(o0, 0);
+        if (bounds[2 * oa] - shift < 0) return IPP_E_RANGE;
+        const int K0 = (bounds[2 * oa] - shift) & ~15;
         int end = K0;
-        for (int o = o0; o < o1; ++o) end = std::max(end, bounds[2 * o] + bounds[2 * o + 1]);
+        for (int o = oa; o < o1; ++o) end = std::max(end, bounds[2 * o] - shift + bounds[2 * o + 1]);
         const int nK = (end - K0 + 63) / 64;
         if (nK > nkb) return IPP_E_RANGE;
         hdr[4 * t] = K0;
@@ -302,11 +313,11 @@ extern "C" int ipp_plan_mfma_from_taps(int32_t in_size, int32_t out_size, int32_
         memset(tb, 0, (size_t)nK * 3 * 64 * 16);
         for (int col = 0; col < 16; ++col) {
             const int o = o0 + col;
-            if (o >= o1) {
-                bias[o] = 0;
+            if (o < oa || o >= o1) {
+                bias[16 * t + col] = 0;
                 continue;
             }
-            const int xmin = bounds[2 * o], cnt = bounds[2 * o + 1];
+            const int xmin = bounds[2 * o] - shift, cnt = bounds[2 * o + 1];
             int64_t sum = 0;
             for (int q = 0; q < cnt; ++q) {
                 const int32_t k = kk[(int64_t)o * ksize + q];
@@ -317,7 +328,7 @@ extern "C" int ipp_plan_mfma_from_taps(int32_t in_size, int32_t out_size, int32_
                 const int lane = 16 * (kin / 16) + col, j = kin % 16;
                 for (int p = 0; p < 3; ++p) tb[((int64_t)(s * 3 + p) * 64 + lane) * 16 + j] = (uint8_t)b[p];
             }
-            bias[o] = (int32_t)((1 << 21) + 128 * sum);
+            bias[16 * t + col] = (int32_t)((1 << 21) + 128 * sum);
         }
         boff += (int64_t)nK * 3 * 64;
     }
@@ -362,8 +373,9 @@ extern "C" int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int3
             const int first = tmp[0], last = tmp[2 * (o - 1)] + tmp[2 * (o - 1) + 1];
             first_last[2 * i] = first;
             first_last[2 * i + 1] = last;
-            const int e = transposed[i] == 2
-                              ? ipp_plan_mfma_from_taps(in, o, ksize, tmp.data(), out + offsets[i])
+            const int e = transposed[i] >= 2
+                              ? ipp_plan_mfma_from_taps(in, o, ksize, tmp.data(), shift_first[i] ? first : 0,
+                                                        transposed[i] - 2, out + offsets[i])
                               : ipp_plan_dot4_from_taps(o, ksize, tmp.data(), shift_first[i] ? first : 0,
                                                         transposed[i], out + offsets[i]);
             if (e) err[t] = e;

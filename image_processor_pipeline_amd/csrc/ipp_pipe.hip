@@ -431,6 +431,123 @@ k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, u
     }
 }
 
+// V pass on MFMA (tap tiles aligned with 16-row background bands: the plan's
+// phase = p.y mod 16) → unpremultiply → blend onto the background, fused with
+// the background copy.  Block = 16 composite rows of one item.  A = taps of
+// the band's 16 overlay rows (lane l: row l&15, T rows 16(l>>4)..+15 of the K
+// step), B = 64 T rows × 16 overlay columns of one channel (four 16-B T groups
+// per lane give all four channels), D lane l = column l&15, rows 4(l>>4)..+3.
+constexpr int VBR = 16;
+
+template <int STORE>
+__global__ void __launch_bounds__(256)
+k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
+                   const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int tiles_y,
+                   int ov_w_max) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t orow[];  // [VBR][ov_w_max]
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / tiles_y;
+    const int ty = b - im * tiles_y;
+    const ipp_paste_desc p = descs[im].p;
+    const int y0 = ty * VBR;
+    if (y0 >= p.bg_h) return;
+    const int nrows = min(VBR, p.bg_h - y0);
+    const int oy_lo = max(0, y0 - p.y), oy_hi = min(p.ov_h, y0 + nrows - p.y);
+    const bool any = oy_lo < oy_hi;  // block-uniform
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+    if (any) {
+        const ipp_resample_desc v = descs[im].v;
+        const int phase = p.y & 15;
+        const int ntiles = (v.out_len + phase + 15) >> 4;
+        const int t = (y0 - p.y + phase) >> 4;  // the band's tap tile
+        const int4* thdr = reinterpret_cast<const int4*>(coefs + v.coef_off);
+        const int32_t* tbias = coefs + v.coef_off + 4 * (int64_t)ntiles;
+        const uint4* tblk = reinterpret_cast<const uint4*>(coefs + v.coef_off + 20 * (int64_t)ntiles);
+        const int4 th = thdr[t];
+        const int ctiles = (p.ov_w + 15) >> 4;
+        const int gstride = v.src_pitch >> 4;  // uint4 per T group row
+        const int x_l = lane & 15;
+        for (int ct = wave; ct < ctiles; ct += 4) {
+            const int x = 16 * ct + x_l;
+            const int xs = min(x, p.ov_w - 1);
+            i32x4 acc[4][3];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) acc[c][q] = i32x4{0, 0, 0, 0};
+#pragma unroll 1
+            for (int ks = 0; ks < th.y; ++ks) {
+                i32x4 a[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) a[q] = __builtin_bit_cast(i32x4, tblk[th.z + (ks * 3 + q) * 64 + lane]);
+                const int G = (th.x + 64 * ks + 16 * (lane >> 4)) >> 2;
+                const uint4* tq = reinterpret_cast<const uint4*>(tmp + v.src_off + (int64_t)G * v.src_pitch) + xs;
+                const uint4 g0 = tq[0], g1 = tq[gstride], g2 = tq[2 * gstride], g3 = tq[3 * gstride];
+                const i32x4 bq[4] = {i32x4{(int)g0.x, (int)g1.x, (int)g2.x, (int)g3.x},
+                                     i32x4{(int)g0.y, (int)g1.y, (int)g2.y, (int)g3.y},
+                                     i32x4{(int)g0.z, (int)g1.z, (int)g2.z, (int)g3.z},
+                                     i32x4{(int)g0.w, (int)g1.w, (int)g2.w, (int)g3.w}};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        acc[c][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[q], bq[c], acc[c][q], 0, 0, 0);
+            }
+            if (x < p.ov_w) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 4 * (lane >> 4) + r;   // band row = tile row
+                    const int o = y0 + row - p.y;           // overlay row
+                    if (o >= oy_lo && o < oy_hi) {
+                        const int32_t bias = tbias[16 * t + row];
+                        uint32_t px = 0;
+#pragma unroll
+                        for (int c = 0; c < 4; ++c)
+                            px |= clip8(bias + acc[c][0][r] + (acc[c][1][r] << 8) + (acc[c][2][r] << 16)) << (8 * c);
+                        orow[row * ov_w_max + x] = unpremultiply(px);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // Phase 2: composite rows = background bytes, blended inside the footprint.
+    // Four 16-B chunks per thread are loaded before any is stored, so each
+    // wave keeps four background reads in flight.
+    const int row_bytes = 3 * p.bg_w;
+    const int chunks = (row_bytes + 15) >> 4;
+    const int total = nrows * chunks;
+    for (int base = threadIdx.x; base < total; base += 4 * 256) {
+        uint32_t w[4][4];
+        int rr[4], c0[4], nb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = base + u * 256;
+            rr[u] = idx / chunks;
+            c0[u] = (idx - rr[u] * chunks) << 4;
+            nb[u] = idx < total ? min(16, row_bytes - c0[u]) : 0;
+            if (nb[u] > 0) {
+                const uint8_t* bp = bg + p.bg_off + (int64_t)(y0 + rr[u]) * p.bg_pitch + c0[u];
+                load16(bp, nb[u], nb[u] == 16 && (reinterpret_cast<uintptr_t>(bp) & 15u) == 0, w[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (nb[u] <= 0) continue;
+            const int o = y0 + rr[u] - p.y;
+            if (any && o >= oy_lo && o < oy_hi && c0[u] + nb[u] > 3 * p.x && c0[u] < 3 * (p.x + p.ov_w)) {
+                const uint32_t* orw = orow + rr[u] * ov_w_max;
+                blend16(w[u], c0[u], nb[u], p.x, p.ov_w, [&](int ox) { return orw[ox]; });
+            }
+            uint8_t* dp = dst + p.dst_off + (int64_t)(y0 + rr[u]) * p.dst_pitch + c0[u];
+            store16<STORE>(dp, nb[u], nb[u] == 16 && (reinterpret_cast<uintptr_t>(dp) & 15u) == 0, w[u]);
+        }
+    }
+}
+
 template <int NR, bool ZONES, int CN>
 void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                   const ipp_pipe_desc* descs, int fmt, int ty, const ipp_hsv_params& hp) {
@@ -507,9 +624,31 @@ extern "C" int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* c
 
 extern "C" int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst, const int32_t* coefs,
                                const ipp_pipe_desc* descs, int32_t n_images, int32_t bg_w, int32_t bg_h,
-                               void* stream) {
+                               int32_t max_ov_w, int32_t tap_format, void* stream) {
     if (n_images == 0) return IPP_OK;
     if (!tmp || !bg || !dst || !coefs || !descs || n_images < 0 || bg_w <= 0 || bg_h <= 0) return IPP_E_ARG;
+    if (tap_format == IPP_TAPS_MFMA) {
+        if (max_ov_w <= 0 || max_ov_w > bg_w) return IPP_E_ARG;
+        const size_t sm = (size_t)VBR * max_ov_w * sizeof(uint32_t);
+        const int tyb = (bg_h + VBR - 1) / VBR;
+        const int64_t nb = (int64_t)tyb * n_images;
+        if (nb >= INT32_MAX || sm > 64 * 1024) return IPP_E_ARG;
+        const dim3 grid((uint32_t)nb);
+        hipStream_t st = (hipStream_t)stream;
+        static const int pol = [] {
+            const char* e = getenv("IPP_VB_STORE");
+            return e ? atoi(e) : 2;
+        }();
+        if (pol == 0)
+            hipLaunchKernelGGL(k_pipe_vblend_mfma<0>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
+        else if (pol == 1)
+            hipLaunchKernelGGL(k_pipe_vblend_mfma<1>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
+        else
+            hipLaunchKernelGGL(k_pipe_vblend_mfma<2>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
+        IPP_CHECK_LAUNCH();
+        return IPP_OK;
+    }
+    if (tap_format != IPP_TAPS_DOT4) return IPP_E_ARG;
     const size_t shmem = (size_t)VR * bg_w * sizeof(uint32_t);
     if (shmem > 160 * 1024) return IPP_E_ARG;
     const int ty = (bg_h + VR - 1) / VR;

@@ -73,7 +73,8 @@ class PipePlan:
     bg_h: int
     algo_bytes_hpass: int = 0
     algo_bytes_vblend: int = 0
-    tap_format: int = 0                   # IPP_TAPS_DOT4 / IPP_TAPS_MFMA (H pass)
+    tap_format: int = 0                   # IPP_TAPS_DOT4 / IPP_TAPS_MFMA (H and V passes)
+    max_ov_w: int = 1
 
 
 def draw_params(n: int, src_hw: Tuple[int, int], bg_hw: Tuple[int, int], n_bg: int, cfg: PipeConfig,
@@ -172,8 +173,10 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     ngs = np.array([lib.ipp_plan_dot4_stride(int(k)) for k in ks], np.int64)
     mfma = TAPS == "mfma"
     # H axes (even j): mfma tiles or transposed dot4; V axes: row-major dot4
-    transp = np.array([(2 if mfma else 1) if j % 2 == 0 else 0 for j in range(m)], np.int32)
-    sizes = np.array([lib.ipp_plan_mfma_size(int(a_in[j]), int(a_out[j]), int(ks[j])) if transp[j] == 2
+    # (V axes in mfma form: tiles aligned with 16-row background bands, phase = y mod 16)
+    transp = np.array([(2 if mfma else 1) if j % 2 == 0 else ((2 + params[j // 2].y % 16) if mfma else 0)
+                       for j in range(m)], np.int32)
+    sizes = np.array([lib.ipp_plan_mfma_size(int(a_in[j]), int(a_out[j]), int(ks[j])) if transp[j] >= 2
                       else 4 * int(a_out[j]) * (1 + int(ngs[j])) for j in range(m)], np.int64)
     sizes = (sizes + 3) // 4 * 4          # 16-B aligned axis blocks
     offs = np.zeros(m, np.int64)
@@ -197,7 +200,11 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
         else:
             y0, y1 = 0, rh
         rows = y1 - y0
-        groups = ((rows + 15) // 16) * 4 + int(ngs[jv]) + 1   # + V-pass over-read pad
+        if mfma:   # V tiles read up to 64·nK rows past their 16-aligned start
+            nkb = lib.ipp_plan_mfma_nk_bound(int(a_in[jv]), int(a_out[jv]), int(ks[jv]))
+            groups = (((rows + 15) // 16) * 16 + 64 * nkb + 16) // 4
+        else:
+            groups = ((rows + 15) // 16) * 4 + int(ngs[jv]) + 1   # + V-pass over-read pad
         pitch = 16 * nw_
         h = d[i]["h"]
         h["dst_off"] = tmp_off
@@ -230,7 +237,8 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     d = d[order]
     hsv = G.hsv_params(cfg.hsv_ranges, cfg.zones, cfg.use_gimp_scale, bgr=False)
     return PipePlan(d, coefs, hsv, params, cut_dims, ov_dims, max(tmp_off, 256), max_out_w, max_rows, bw, bh,
-                    algo_h, algo_v, N.IPP_TAPS_MFMA if mfma else N.IPP_TAPS_DOT4)
+                    algo_h, algo_v, N.IPP_TAPS_MFMA if mfma else N.IPP_TAPS_DOT4,
+                    max(w for _, w in ov_dims))
 
 
 class PipeRunner:
@@ -253,8 +261,8 @@ class PipeRunner:
     def vblend(self, bgs: torch.Tensor, out: torch.Tensor) -> None:
         p = self.plan
         N.check(self.lib.ipp_pipe_vblend(self.tmp.data_ptr(), bgs.data_ptr(), out.data_ptr(), self.coefs.data_ptr(),
-                                         self.descs.data_ptr(), len(p.descs), p.bg_w, p.bg_h,
-                                         _stream(self.device)), "ipp_pipe_vblend")
+                                         self.descs.data_ptr(), len(p.descs), p.bg_w, p.bg_h, p.max_ov_w,
+                                         p.tap_format, _stream(self.device)), "ipp_pipe_vblend")
 
     def run(self, src: torch.Tensor, bgs: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         for t, name in ((src, "src"), (bgs, "bgs"), (out, "out")):

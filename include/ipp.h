@@ -192,9 +192,14 @@ int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                    const ipp_pipe_desc* descs, int32_t n_images,
                    int32_t max_out_w, int32_t max_rows, int32_t src_cn,
                    const ipp_hsv_params* hsv, int32_t tap_format, void* stream);
+/* tap_format: IPP_TAPS_DOT4 (V axes planned with transposed = 0) or
+ * IPP_TAPS_MFMA (V axes planned with transposed = 2 + (p.y mod 16), i.e. tap
+ * tiles aligned with 16-row background bands); max_ov_w bounds the overlay
+ * widths (MFMA path). */
 int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
                     const int32_t* coefs, const ipp_pipe_desc* descs, int32_t n_images,
-                    int32_t bg_w, int32_t bg_h, void* stream);
+                    int32_t bg_w, int32_t bg_h, int32_t max_ov_w, int32_t tap_format,
+                    void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* K10-K13: pixels_isolés.keep_largest_component                             */
@@ -275,13 +280,15 @@ int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int32_t* out_si
                        const int32_t* identity, const int32_t* shift_first,
                        const int32_t* transposed, const int64_t* offsets, int32_t* out,
                        int32_t* first_last, int32_t n_threads);
-/* MFMA tile format of an H axis for the fused pipe (v_mfma_i32_16x16x64_i8;
- * see ipp_host.cpp): size bound in int32 for (in, out, ksize), and the
- * conversion from standard Pillow taps.  ipp_plan_pipe_axes writes this
- * format for axes with transposed[i] == 2. */
+/* MFMA tile format of a pipe axis (v_mfma_i32_16x16x64_i8; see ipp_host.cpp):
+ * size bound in int32 for (in, out, ksize), bound on K steps per tile, and the
+ * conversion from standard Pillow taps (input indices minus `shift`, tiles
+ * offset by `phase` outputs).  ipp_plan_pipe_axes writes this format for axes
+ * with transposed[i] = 2 + phase. */
 int64_t ipp_plan_mfma_size(int32_t in_size, int32_t out_size, int32_t ksize);
+int32_t ipp_plan_mfma_nk_bound(int32_t in_size, int32_t out_size, int32_t ksize);
 int ipp_plan_mfma_from_taps(int32_t in_size, int32_t out_size, int32_t ksize,
-                            const int32_t* std_taps, int32_t* out);
+                            const int32_t* std_taps, int32_t shift, int32_t phase, int32_t* out);
 /* ksize for (in_size, out_size) without computing taps. */
 int32_t ipp_plan_lanczos_ksize(double in0, double in1, int32_t out_size);
 

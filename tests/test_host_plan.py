@@ -112,21 +112,26 @@ def test_overlay_size_and_hsv_params():
         G.hsv_params([])
 
 
-@pytest.mark.parametrize("io", [(1100, 230), (1268, 150), (896, 896), (40, 13), (1, 1), (300, 299), (57, 20)])
-def test_mfma_tile_format_is_exact(io):
+@pytest.mark.parametrize("io,shift,phase", [((1100, 230), 0, 0), ((1268, 150), 0, 7), ((896, 896), 0, 0),
+                                            ((40, 13), 0, 3), ((1, 1), 0, 0), ((300, 299), 0, 15), ((57, 20), 0, 0),
+                                            ((1150, 240), 9, 5)])
+def test_mfma_tile_format_is_exact(io, shift, phase):
     """Emulate v_mfma_i32_16x16x64_i8 on the planned B blocks: for every
     output, bias + Σ_p 2^(8p) Σ_s Σ_k (pix[K0+64s+k] ^ 0x80) · B_p[k][col]
     == 2^21 + Σ p·k (the identity the MFMA H pass relies on)."""
     lib = N.load()
     i, o = io
     k, std = G.lanczos_taps(i, o)
+    if shift:
+        std[0:2 * o:2] += shift   # pretend the axis starts `shift` rows later
     size = lib.ipp_plan_mfma_size(i, o, k)
     out = np.zeros(size, np.int32)
-    assert lib.ipp_plan_mfma_from_taps(i, o, k, N.np_ptr(std), N.np_ptr(out)) == 0
-    T = (o + 15) // 16
+    assert lib.ipp_plan_mfma_from_taps(i, o, k, N.np_ptr(std), shift, phase, N.np_ptr(out)) == 0
+    T = (o + phase + 15) // 16
     hdr = out[:4 * T].reshape(T, 4)
     bias = out[4 * T:20 * T]
-    blocks = out[20 * T:].view(np.uint8).view(np.int8).reshape(-1, 64, 16)
+    nblk = int(max(hdr[:, 2] // 64 + hdr[:, 1] * 3))
+    blocks = out[20 * T:20 * T + nblk * 256].view(np.uint8).view(np.int8).reshape(-1, 64, 16)
     rng = np.random.default_rng(5)
     pix = rng.integers(0, 256, i + 256, np.uint8)
     sp = (pix ^ 0x80).view(np.int8).astype(np.int64)
@@ -144,10 +149,11 @@ def test_mfma_tile_format_is_exact(io):
                 a = np.pad(a, (0, 64 - len(a)))
                 acc[p] += a @ Bm
         for col in range(16):
-            oo = 16 * t + col
-            if oo >= o:
+            oo = 16 * t - phase + col
+            if oo < 0 or oo >= o:
+                assert bias[16 * t + col] == 0
                 continue
-            xmin, cnt = std[2 * oo], std[2 * oo + 1]
+            xmin, cnt = std[2 * oo] - shift, std[2 * oo + 1]
             ref = (1 << 21) + int((pix[xmin:xmin + cnt].astype(np.int64) * std[2 * o + oo * k:2 * o + oo * k + cnt]).sum())
-            got = int(bias[oo]) + int(acc[0, col]) + (int(acc[1, col]) << 8) + (int(acc[2, col]) << 16)
+            got = int(bias[16 * t + col]) + int(acc[0, col]) + (int(acc[1, col]) << 8) + (int(acc[2, col]) << 16)
             assert got == ref, (t, col)
