@@ -141,7 +141,7 @@ struct __attribute__((aligned(16))) HpassLds {
 // HSV-tested exactly once.
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 
-template <int NR, bool ZONES, int CN, int FMT>
+template <int NR, bool ZONES, int CN, int FMT, int DBG = 0>
 __global__ void __launch_bounds__(256)
 k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
              const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp) {
@@ -229,7 +229,7 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint32_t p = gather4_pixel<CN>(cur, k);
-                    px[k] = keep_pixel(p, hsv_keep<NR, ZONES>(R, L.sdiv, L.hdiv, p, x + k, y));
+                    px[k] = (DBG & 1) ? (p | 0xFF000000u) : keep_pixel(p, hsv_keep<NR, ZONES>(R, L.sdiv, L.hdiv, p, x + k, y));
                 }
             } else {
                 // all-fill wave: HSV of black is constant, only zones vary
@@ -301,7 +301,7 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
             // B = 64 columns × 16 outputs of one tap byte plane.  D lane l =
             // output l&15, rows 4(l>>4)..+3 = exactly one 16-B T group.
             const int t = s0 + wave;
-            if (t < s1) {
+            if (!(DBG & 2) && t < s1) {
                 const int4 th = hdr[t];
                 i32x4 acc[4][3];
 #pragma unroll
@@ -439,7 +439,7 @@ k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, u
 // per lane give all four channels), D lane l = column l&15, rows 4(l>>4)..+3.
 constexpr int VBR = 16;
 
-template <int STORE>
+template <int STORE, int DBG = 0>
 __global__ void __launch_bounds__(256)
 k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
                    const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int tiles_y,
@@ -453,7 +453,7 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
     if (y0 >= p.bg_h) return;
     const int nrows = min(VBR, p.bg_h - y0);
     const int oy_lo = max(0, y0 - p.y), oy_hi = min(p.ov_h, y0 + nrows - p.y);
-    const bool any = oy_lo < oy_hi;  // block-uniform
+    const bool any = (DBG & 2) ? false : oy_lo < oy_hi;  // block-uniform
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
@@ -531,7 +531,11 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
             nb[u] = idx < total ? min(16, row_bytes - c0[u]) : 0;
             if (nb[u] > 0) {
                 const uint8_t* bp = bg + p.bg_off + (int64_t)(y0 + rr[u]) * p.bg_pitch + c0[u];
-                load16(bp, nb[u], nb[u] == 16 && (reinterpret_cast<uintptr_t>(bp) & 15u) == 0, w[u]);
+                if (DBG & 1) {
+                    w[u][0] = w[u][1] = w[u][2] = w[u][3] = (uint32_t)c0[u];
+                } else {
+                    load16(bp, nb[u], nb[u] == 16 && (reinterpret_cast<uintptr_t>(bp) & 15u) == 0, w[u]);
+                }
             }
         }
 #pragma unroll
@@ -551,7 +555,17 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
 template <int NR, bool ZONES, int CN>
 void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                   const ipp_pipe_desc* descs, int fmt, int ty, const ipp_hsv_params& hp) {
-    if (fmt == IPP_TAPS_MFMA)
+    static const int dbg = [] {
+        const char* e = getenv("IPP_DBG_HPASS");  // diagnostics (wrong output): 1 no HSV, 2 no H taps, 3 neither
+        return e ? atoi(e) : 0;
+    }();
+    if (fmt == IPP_TAPS_MFMA && dbg == 1)
+        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
+    else if (fmt == IPP_TAPS_MFMA && dbg == 2)
+        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 2>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
+    else if (fmt == IPP_TAPS_MFMA && dbg == 3)
+        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 3>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
+    else if (fmt == IPP_TAPS_MFMA)
         hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
     else
         hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 0>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
@@ -643,6 +657,12 @@ extern "C" int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* d
             hipLaunchKernelGGL(k_pipe_vblend_mfma<0>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
         else if (pol == 1)
             hipLaunchKernelGGL(k_pipe_vblend_mfma<1>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
+        else if (pol == 9)  // diagnostics (wrong output): no background reads
+            hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 1>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
+        else if (pol == 10)  // ... no V pass
+            hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 2>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
+        else if (pol == 11)  // ... stores only
+            hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 3>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
         else
             hipLaunchKernelGGL(k_pipe_vblend_mfma<2>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
         IPP_CHECK_LAUNCH();
