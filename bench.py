@@ -46,8 +46,6 @@ def parse():
     ap.add_argument("--backgrounds", type=int, default=16)
     ap.add_argument("--workload", choices=["pipe5", "rotflip", "video4k"], default="pipe5")
     ap.add_argument("--frames", type=int, default=256, help="video4k: 3840x2160 frames per GPU")
-    ap.add_argument("--chunk", type=int, default=int(os.environ.get("IPP_CHUNK", "0")),
-                    help="pipe5: items per hpass/vblend pair (0 = whole batch)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=192)
@@ -129,15 +127,11 @@ def main():
         if world > 1:
             dist.broadcast(bgs, src=0)  # the one exchange step: shared assets over xGMI
         cfg = fused.PipeConfig()
-        plan = fused.plan_pipe((S, S), B, (S, S), K, cfg, seed=args.seed * 7919, item_range=(start, stop),
-                               chunk=args.chunk)
+        plan = fused.plan_pipe((S, S), B, (S, S), K, cfg, seed=args.seed * 7919, item_range=(start, stop))
         runner = fused.PipeRunner(plan, dev)
         out = torch.empty((B, S, S, 3), dtype=torch.uint8, device=dev)
         algo = {"ipp_pipe_hpass": plan.algo_bytes_hpass, "ipp_pipe_vblend": plan.algo_bytes_vblend}
-        launches = []
-        for k0, k1 in runner.chunks():
-            launches.append(("ipp_pipe_hpass", lambda k0=k0, k1=k1: runner.hpass(src, k0, k1)))
-            launches.append(("ipp_pipe_vblend", lambda k0=k0, k1=k1: runner.vblend(bgs, out, k0, k1)))
+        launches = [("ipp_pipe_hpass", lambda: runner.hpass(src)), ("ipp_pipe_vblend", lambda: runner.vblend(bgs, out))]
         workload = "5-stage pipe: crop(64px)->rotate(NEAREST,expand,bbox)->flip->HSV mask(4 ref ranges)->LANCZOS+paste"
     elif args.workload == "video4k":
         from image_processor_pipeline_amd import video_chain
