@@ -7,7 +7,7 @@ CSRC := $(PKG)/csrc
 SRCS := $(CSRC)/ipp_gather.hip $(CSRC)/ipp_hsv.hip $(CSRC)/ipp_resample.hip $(CSRC)/ipp_pipe.hip \
         $(CSRC)/ipp_ccl.hip
 HOST_SRCS := $(CSRC)/ipp_host.cpp
-HDRS := include/ipp.h $(CSRC)/ipp_device.h $(CSRC)/ipp_hsv.h
+HDRS := include/ipp.h $(wildcard $(CSRC)/*.h)
 OBJDIR := build/obj
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS)) $(OBJDIR)/ipp_host.o
 LIB := $(PKG)/libipp.so

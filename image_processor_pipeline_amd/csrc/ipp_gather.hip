@@ -13,6 +13,7 @@
 // 64×16 output tile.  Blocks are remapped so the tiles of one image share an
 // XCD (its source stays in that XCD's L2).
 #include "ipp_device.h"
+#include "ipp_sampler.h"
 
 namespace {
 
@@ -22,53 +23,68 @@ struct TileGrid {
     int tiles_x, tiles_y;
 };
 
-__device__ __forceinline__ uint32_t gather_pixel(const uint8_t* __restrict__ src, const ipp_gather_desc& d,
-                                                 uint32_t rowx, uint32_t rowy, int X) {
-    int32_t xx = (int32_t)(rowx + (uint32_t)X * (uint32_t)d.a0);
-    int32_t yy = (int32_t)(rowy + (uint32_t)X * (uint32_t)d.a3);
-    int xin = xx >> 16, yin = yy >> 16;
-    if ((unsigned)xin >= (unsigned)d.in_w || (unsigned)yin >= (unsigned)d.in_h) return 0u;
-    int sx = d.in_x0 + xin, sy = d.in_y0 + yin;
-    const uint8_t* p = src + d.src_off + (int64_t)sy * d.src_pitch;
-    if (d.src_cn == 4) return *reinterpret_cast<const uint32_t*>(p + 4 * sx);
-    bool wide_ok = (sy < d.src_h - 1) || (sx < d.src_w - 1);
-    return load_rgb_opaque(p + 3 * sx, wide_ok);
+// One 64×16 output tile per block, branch-free gathers.  Two lane maps:
+//   PATCH: wave w gathers the 16×16 patch at columns 16w.. (lane: row lane>>2,
+//          4 pixels at 4·(lane&3)) — each load instruction's addresses fall in
+//          a compact source patch — then the tile is restaged through LDS so
+//          every wave stores 4 full rows (256 B per row per instruction);
+//   ROWS:  wave w covers rows 4w..4w+3 directly (16 lanes × 4 pixels per row).
+template <int CN, bool PATCH>
+__device__ __forceinline__ void rotate_tile(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                            const ipp_gather_desc& d, int tx, int ty, uint4* stage) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int gy, gx;  // gathered pixel block (row, first column) of this thread
+    if (PATCH) {
+        gy = lane >> 2;
+        gx = 16 * wave + 4 * (lane & 3);
+    } else {
+        gy = (int)(threadIdx.x >> 4);
+        gx = 4 * (int)(threadIdx.x & 15);
+    }
+    if (ty * TILE_H >= d.out_h || tx * TILE_W >= d.out_w) return;  // block-uniform
+    const Sampler S = make_sampler(src, d);
+    const int y = ty * TILE_H + gy, x0 = tx * TILE_W + gx;
+    Gather4<CN> G;
+    gather4_issue<CN>(S, (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1 + (uint32_t)x0 * (uint32_t)S.b0,
+                      (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4 + (uint32_t)x0 * (uint32_t)S.b3, G);
+    uint4 px;
+    px.x = gather4_pixel<CN>(G, 0);
+    px.y = gather4_pixel<CN>(G, 1);
+    px.z = gather4_pixel<CN>(G, 2);
+    px.w = gather4_pixel<CN>(G, 3);
+    int sy = y, sx0 = x0;
+    if (PATCH) {  // restage: store pattern = ROWS map
+        stage[gy * 16 + (gx >> 2)] = px;
+        __syncthreads();
+        const int ry = (int)(threadIdx.x >> 4), rx = 4 * (int)(threadIdx.x & 15);
+        px = stage[ry * 16 + (rx >> 2)];
+        sy = ty * TILE_H + ry;
+        sx0 = tx * TILE_W + rx;
+    }
+    if (sy >= d.out_h || sx0 >= d.out_w) return;
+    uint8_t* o = dst + d.dst_off + (int64_t)sy * d.dst_pitch + 4 * sx0;
+    if (sx0 + 4 <= d.out_w && ((reinterpret_cast<uintptr_t>(o) & 15u) == 0)) {
+        *reinterpret_cast<uint4*>(o) = px;
+    } else {
+        const uint32_t pv[4] = {px.x, px.y, px.z, px.w};
+        for (int k = 0; k < 4; ++k)
+            if (sx0 + k < d.out_w) reinterpret_cast<uint32_t*>(o)[k] = pv[k];
+    }
 }
 
+template <bool PATCH>
 __global__ void __launch_bounds__(256)
 k_rotate_flip_nearest(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                       const ipp_gather_desc* __restrict__ descs, int tiles_x, int tiles_y) {
-    const uint32_t nblk = gridDim.x;
-    const uint32_t b = xcd_remap(blockIdx.x, nblk);
+    __shared__ uint4 stage[PATCH ? TILE_H * 16 : 1];
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int per_img = tiles_x * tiles_y;
     const int img = b / per_img;
     const int t = b - img * per_img;
     const int ty = t / tiles_x, tx = t - ty * tiles_x;
     const ipp_gather_desc d = descs[img];
-    const int y = ty * TILE_H + (int)(threadIdx.x >> 4);
-    const int x0 = tx * TILE_W + (int)(threadIdx.x & 15) * PX_PER_THREAD;
-    if (y >= d.out_h || x0 >= d.out_w) return;
-
-    const int fy = (d.flip & 2) ? d.out_h - 1 - y : y;
-    const int Y = d.off_y + fy;
-    const uint32_t rowx = (uint32_t)d.a2 + (uint32_t)Y * (uint32_t)d.a1;
-    const uint32_t rowy = (uint32_t)d.a5 + (uint32_t)Y * (uint32_t)d.a4;
-    uint32_t px[PX_PER_THREAD];
-#pragma unroll
-    for (int k = 0; k < PX_PER_THREAD; ++k) {
-        const int x = x0 + k;
-        const int fx = (d.flip & 1) ? d.out_w - 1 - x : x;
-        px[k] = (x < d.out_w) ? gather_pixel(src, d, rowx, rowy, d.off_x + fx) : 0u;
-    }
-    uint8_t* o = dst + d.dst_off + (int64_t)y * d.dst_pitch + 4 * x0;
-    const bool full = (x0 + PX_PER_THREAD <= d.out_w);
-    if (full && ((reinterpret_cast<uintptr_t>(o) & 15u) == 0)) {
-        *reinterpret_cast<uint4*>(o) = make_uint4(px[0], px[1], px[2], px[3]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < PX_PER_THREAD; ++k)
-            if (x0 + k < d.out_w) reinterpret_cast<uint32_t*>(o)[k] = px[k];
-    }
+    if (d.src_cn == 4) rotate_tile<4, PATCH>(src, dst, d, tx, ty, stage);  // block-uniform
+    else rotate_tile<3, PATCH>(src, dst, d, tx, ty, stage);
 }
 
 // Window copy with optional mirror, any bytes-per-pixel (1..4).  Each thread
@@ -202,8 +218,16 @@ extern "C" int ipp_rotate_flip_nearest(const uint8_t* src, uint8_t* dst, const i
     const int tx = (max_out_w + TILE_W - 1) / TILE_W, ty = (max_out_h + TILE_H - 1) / TILE_H;
     const int64_t blocks = (int64_t)tx * ty * n_images;
     if (!grid_ok(blocks)) return IPP_E_ARG;
-    hipLaunchKernelGGL(k_rotate_flip_nearest, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
-                       src, dst, descs, tx, ty);
+    static const int map = [] {
+        const char* e = getenv("IPP_GATHER_MAP");  // 0 rows, 1 patch + LDS restage
+        return e ? atoi(e) : 1;
+    }();
+    if (map == 0)
+        hipLaunchKernelGGL(k_rotate_flip_nearest<false>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
+                           src, dst, descs, tx, ty);
+    else
+        hipLaunchKernelGGL(k_rotate_flip_nearest<true>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
+                           src, dst, descs, tx, ty);
     IPP_CHECK_LAUNCH();
     return IPP_OK;
 }

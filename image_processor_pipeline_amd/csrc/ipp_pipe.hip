@@ -22,6 +22,7 @@
 // rows] bytes (16 B per (g, x')), values XOR 0x80, so the V pass reads one
 // dwordx4 per 4 taps per pixel.  T rows are M rows [line0, line0 + lines).
 #include "ipp_hsv.h"
+#include "ipp_sampler.h"
 
 namespace {
 
@@ -47,71 +48,6 @@ __device__ __forceinline__ int32_t sdot4(uint32_t a, uint32_t b, int32_t c) {
 
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
     return __builtin_amdgcn_perm(hi, lo, sel);
-}
-
-// Source sampling for M pixel (x, y): flip + bbox offset folded into the 16.16
-// map so xx = B2 + y*B1 + x*B0 (int32 wrap-around arithmetic, as Pillow).
-struct Sampler {
-    const uint8_t* base;  // source pixel (in_x0, in_y0)
-    uint32_t pitch, lim;  // lim: last byte offset from base where a dword load fits
-    int32_t b0, b1, b2, b3, b4, b5;
-    int32_t in_w, in_h;
-};
-
-__device__ __forceinline__ Sampler make_sampler(const uint8_t* src, const ipp_gather_desc& g) {
-    Sampler s;
-    s.base = src + g.src_off + (int64_t)g.in_y0 * g.src_pitch + (int64_t)g.in_x0 * g.src_cn;
-    s.pitch = (uint32_t)g.src_pitch;
-    const int64_t avail = (int64_t)(g.src_h - g.in_y0) * g.src_pitch - (int64_t)g.in_x0 * g.src_cn;
-    s.lim = (uint32_t)(avail - 4);
-    const int sgx = (g.flip & 1) ? -1 : 1, sgy = (g.flip & 2) ? -1 : 1;
-    const uint32_t sx0 = (uint32_t)(g.off_x + ((g.flip & 1) ? g.out_w - 1 : 0));
-    const uint32_t sy0 = (uint32_t)(g.off_y + ((g.flip & 2) ? g.out_h - 1 : 0));
-    s.b0 = (int32_t)((uint32_t)sgx * (uint32_t)g.a0);
-    s.b1 = (int32_t)((uint32_t)sgy * (uint32_t)g.a1);
-    s.b2 = (int32_t)((uint32_t)g.a2 + sy0 * (uint32_t)g.a1 + sx0 * (uint32_t)g.a0);
-    s.b3 = (int32_t)((uint32_t)sgx * (uint32_t)g.a3);
-    s.b4 = (int32_t)((uint32_t)sgy * (uint32_t)g.a4);
-    s.b5 = (int32_t)((uint32_t)g.a5 + sy0 * (uint32_t)g.a4 + sx0 * (uint32_t)g.a3);
-    s.in_w = g.in_w;
-    s.in_h = g.in_h;
-    return s;
-}
-
-// Four horizontally adjacent M pixels: issue the four (branch-free) loads.
-// Invalid lanes read the window origin; `valid` masks them afterwards.
-template <int CN>
-struct Gather4 {
-    uint32_t raw[4];
-    uint32_t sh[4];   // right shift (0 or 8) for a clamped tail load
-    uint32_t valid;   // bit k: pixel k inside the source
-};
-
-template <int CN>
-__device__ __forceinline__ void gather4_issue(const Sampler& S, uint32_t xx, uint32_t yy, Gather4<CN>& G) {
-    G.valid = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int xin = (int32_t)xx >> 16, yin = (int32_t)yy >> 16;
-        const bool ok = ((uint32_t)xin < (uint32_t)S.in_w) & ((uint32_t)yin < (uint32_t)S.in_h);
-        const uint32_t off_any = (uint32_t)__umul24(yin, S.pitch) + (uint32_t)__umul24(xin, CN);
-        uint32_t off = ok ? off_any : 0u;
-        if (CN == 3) {
-            const uint32_t offc = min(off, S.lim);
-            G.sh[k] = (off - offc) << 3;
-            off = offc;
-        }
-        G.raw[k] = *reinterpret_cast<const ipp_u32_unaligned*>(S.base + off);
-        G.valid |= (ok ? 1u : 0u) << k;
-        xx += (uint32_t)S.b0;
-        yy += (uint32_t)S.b3;
-    }
-}
-
-template <int CN>
-__device__ __forceinline__ uint32_t gather4_pixel(const Gather4<CN>& G, int k) {
-    const uint32_t p = CN == 3 ? (G.raw[k] >> G.sh[k]) : G.raw[k];
-    return ((G.valid >> k) & 1u) ? (p | 0xFF000000u) : 0u;
 }
 
 // Transpose 4 packed pixels (RGBA each) into 4 channel-planar dwords.
@@ -213,7 +149,8 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
         int cg0 = wave * 4;
         if (cg0 < ng4) {
             const int x = c0 + 4 * (cg0 + (lane & 3));
-            gather4_issue<CN>(S, rowx + (uint32_t)x * (uint32_t)S.b0, rowy + (uint32_t)x * (uint32_t)S.b3, nxt);
+            if (DBG & 4) { nxt.valid = 15u; for (int k = 0; k < 4; ++k) { nxt.raw[k] = x * 2654435761u + k; nxt.sh[k] = 0; } }
+            else gather4_issue<CN>(S, rowx + (uint32_t)x * (uint32_t)S.b0, rowy + (uint32_t)x * (uint32_t)S.b3, nxt);
         }
         for (; cg0 < ng4; cg0 += 16) {
             cur = nxt;
@@ -221,7 +158,8 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
             const int x = c0 + 4 * cg;
             if (cg0 + 16 < ng4) {
                 const int xn = x + 64;
-                gather4_issue<CN>(S, rowx + (uint32_t)xn * (uint32_t)S.b0, rowy + (uint32_t)xn * (uint32_t)S.b3, nxt);
+                if (DBG & 4) { nxt.valid = 15u; for (int k = 0; k < 4; ++k) { nxt.raw[k] = xn * 2654435761u + k + y; nxt.sh[k] = 0; } }
+                else gather4_issue<CN>(S, rowx + (uint32_t)xn * (uint32_t)S.b0, rowy + (uint32_t)xn * (uint32_t)S.b3, nxt);
             }
             const bool active = (cg < ng4) && (r < nrows);
             uint32_t px[4];
@@ -565,6 +503,10 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
         hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 2>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
     else if (fmt == IPP_TAPS_MFMA && dbg == 3)
         hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 3>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
+    else if (fmt == IPP_TAPS_MFMA && dbg == 4)
+        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 4>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
+    else if (fmt == IPP_TAPS_MFMA && dbg == 7)
+        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 7>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
     else if (fmt == IPP_TAPS_MFMA)
         hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
     else
