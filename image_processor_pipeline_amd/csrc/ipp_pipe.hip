@@ -292,6 +292,401 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
     }
 }
 
+// ---------------------------------------------------------------------------
+// H pass v2 (MFMA taps): table-driven HSV test and buffer-load gathers.
+//
+// The M pixel is (R, G, B) of the source or black outside it (rotations.py
+// fills with transparent black and filtres_liste.py:84 reads the file back
+// with cv2.imread, which drops alpha, so fill and real black pixels are
+// indistinguishable from the HSV step on).  Hence:
+//   * gathers go through a buffer resource whose range check returns 0 for the
+//     out-of-window offset 0xFFFFFFFF — no validity bits, no value masking;
+//   * the inRange union is decided by three LDS mask tables instead of packed
+//     compares: bit k of vm[v], sm[s], hm[h + 32] says range k holds on that
+//     channel, so  excluded ⟺ vm[v] & sm[s] & hm[h + 32] (& zone bits) ≠ 0.
+//     h + 32 falls out of the rounding constant (2048 + 32·4096), and hm folds
+//     OpenCV's h < 0 → h + 180 wrap into the table.
+// ---------------------------------------------------------------------------
+template <int NR>
+struct MaskType { typedef uint8_t T; };
+template <>
+struct MaskType<IPP_MAX_HSV_RANGES> { typedef uint16_t T; };
+
+constexpr int HMN = 192;  // hm entries: h + 32 ∈ [2, 182]
+
+template <int NR>
+struct __attribute__((aligned(16))) Hpass2Lds {
+    typedef typename MaskType<NR>::T MT;
+    uint8_t win[4][HR][WSTRIDE];   // planar window ring, bytes p ^ 0x80
+    uint32_t sv[256];              // sdiv[v]
+    int32_t hd[256];               // hdiv[diff]
+    MT vm[256], sm[256], hm[HMN];  // per-channel range masks
+};
+
+// M pixel → window byte quad (p | α 255) ^ 0x80 when kept, 0x80808080 (transparent black) when excluded.
+template <int NR, bool ZONES>
+__device__ __forceinline__ uint32_t hsv2_px(const Hpass2Lds<NR>& L, uint32_t raw, uint32_t zbits) {
+    const uint32_t r = raw & 0xFFu, g = (raw >> 8) & 0xFFu, b = (raw >> 16) & 0xFFu;
+    const uint32_t v = max(max(r, g), b);
+    const uint32_t d = v - min(min(r, g), b);
+    const uint32_t s = mad_u24(d, L.sv[v], 2048u) >> 12;
+    // OpenCV's hue numerator: v==r ? g-b : v==g ? b-r+2d : r-g+4d
+    const int nr = (int)g - (int)b, ng = (int)b - (int)r + 2 * (int)d, nb = (int)r - (int)g + 4 * (int)d;
+    int n = (v == g) ? ng : nb;
+    n = (v == r) ? nr : n;
+    const uint32_t hi = (uint32_t)mad_i24(n, L.hd[d], 2048 + (32 << 12)) >> 12;
+    uint32_t ex = (uint32_t)L.vm[v] & (uint32_t)L.sm[s] & (uint32_t)L.hm[hi];
+    if (ZONES) ex &= zbits;
+    const uint32_t t = (raw | 0xFF000000u) ^ 0x80808080u;
+    return ex ? 0x80808080u : t;
+}
+
+// Per-block state of the v2 H pass.
+struct Hp2Block {
+    __amdgpu_buffer_rsrc_t rs;  // source window (records = bytes to the image end)
+    uint32_t lim;               // CLAMP: last byte offset where a dword fits
+    uint32_t rowx, rowy;        // 16.16 source position of column 0 of the lane's row
+    int32_t b0, b3, pitch, in_w, in_h;
+    int32_t xlo, xhi;           // band's valid M columns ⊆ [xlo, xhi] (conservative)
+};
+
+// 4 gathered pixels of lane group x .. x+3 (raw dwords; 0 outside the window).
+struct Raw4 {
+    uint32_t p[4];
+    uint32_t sh[4];
+    bool any;
+};
+
+// Gathers of one step: xx/yy = 16.16 source position of the lane's first
+// pixel (its next three are +b0/+b3 apart).
+template <int CN, bool CLAMP, int DBG = 0>
+__device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32_t yy, int x, Raw4& o) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int xin = (int32_t)xx >> 16, yin = (int32_t)yy >> 16;
+        const bool ok = ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h);
+        uint32_t off = (uint32_t)__mul24(yin, B.pitch) + (uint32_t)__umul24((uint32_t)xin, (uint32_t)CN);
+        if (CLAMP) {
+            const uint32_t offc = min(off, B.lim);
+            o.sh[k] = ok ? (off - offc) << 3 : 0u;
+            off = offc;
+        }
+        if (DBG & 1) off = (uint32_t)((x >> 6) * 768 + (threadIdx.x & 63) * 3 + k * 192 + (threadIdx.x >> 8) * 3072);
+        off = ok ? off : 0xFFFFFFFFu;
+        o.p[k] = __builtin_amdgcn_raw_buffer_load_b32(B.rs, off, 0, 0);
+        any |= ok;
+        xx += (uint32_t)B.b0;
+        yy += (uint32_t)B.b3;
+    }
+    o.any = any;
+}
+
+// One chunk of ≤ 4 output tiles whose input window fits the ring.
+struct Hp2Chunk {
+    int s0, s1;   // tiles [s0, s1)
+    int c0;       // first M column not yet in the ring
+    int ng4;      // new 4-column groups
+    int nsteps;   // this wave's phase-1 steps (16 groups per step over the block)
+};
+
+__device__ __forceinline__ Hp2Chunk hp2_chunk(const int4* hdr, int s0, int ntiles, int& filled, int wave) {
+    Hp2Chunk c;
+    c.s0 = s0;
+    const int W0 = hdr[s0].x;
+    int s1 = min(s0 + 4, ntiles), W1;
+    for (;;) {
+        W1 = W0;
+        for (int t = s0; t < s1; ++t) W1 = max(W1, hdr[t].x + 64 * hdr[t].y);
+        if (s1 - s0 == 1 || W1 - W0 <= RING) break;
+        --s1;
+    }
+    c.s1 = s1;
+    c.c0 = max(filled, W0);
+    c.ng4 = max(0, (W1 - c.c0) >> 2);
+    c.nsteps = c.ng4 > wave * 4 ? (c.ng4 - wave * 4 + 15) >> 4 : 0;
+    filled = max(filled, W1);
+    return c;
+}
+
+template <int NR, bool ZONES, int CN, bool CLAMP, int DBG = 0>
+__device__ __forceinline__ void hpass2_body(Hpass2Lds<NR>& L, const Hp2Block& B, uint8_t* __restrict__ tmp,
+                                            const int32_t* __restrict__ coefs, const ipp_resample_desc& h,
+                                            int row0, int nrows, const int32_t* zc0, const int32_t* zcw,
+                                            uint32_t zrow, uint32_t fill) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane >> 2;
+    const int ntiles = (h.out_len + 15) >> 4;
+    const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
+    const int32_t* tbias = coefs + h.coef_off + 4 * (int64_t)ntiles;
+    const uint4* tblk = reinterpret_cast<const uint4*>(coefs + h.coef_off + 20 * (int64_t)ntiles);
+    const uint32_t sx = 64u * (uint32_t)B.b0, sy = 64u * (uint32_t)B.b3;  // per-step advance
+
+    int filled = hdr[0].x;  // ring holds M columns [.., filled)
+    Hp2Chunk ck = hp2_chunk(hdr, 0, ntiles, filled, wave);
+    // Lane's first column of step 0 and its source position.
+    auto lane_x = [&](const Hp2Chunk& c) { return c.c0 + 4 * (wave * 4 + (lane & 3)); };
+    int xl = lane_x(ck);
+    uint32_t xxl = B.rowx + (uint32_t)xl * (uint32_t)B.b0, yyl = B.rowy + (uint32_t)xl * (uint32_t)B.b3;
+    Raw4 RA, RB, RC;
+    if (CLAMP) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) RA.sh[k] = RB.sh[k] = RC.sh[k] = 0u;
+    }
+    // A step = 16 columns of 16 rows per wave; steps wholly outside the band's
+    // valid columns are all fill: no gathers, no HSV, constant window bytes.
+    auto step_live = [&](const Hp2Chunk& c, int st) {
+        const int xs = c.c0 + 16 * wave + 64 * st;
+        return xs + 15 >= B.xlo && xs <= B.xhi;
+    };
+    auto issue = [&](const Hp2Chunk& c, int st, uint32_t xx, uint32_t yy, int x, Raw4& o) {
+        if (step_live(c, st)) hp2_issue<CN, CLAMP, DBG>(B, xx, yy, x, o);
+        else o.any = false;
+    };
+    if (ck.nsteps > 0) issue(ck, 0, xxl, yyl, xl, RA);
+    if (ck.nsteps > 1) issue(ck, 1, xxl + sx, yyl + sy, xl + 64, RB);
+
+    for (;;) {
+        // This wave's tile taps for the first K step, in flight during phase 1.
+        const int t = ck.s0 + wave;
+        const bool has_tile = !(DBG & 4) && t < ck.s1;
+        int4 th = make_int4(0, 0, 0, 0);
+        uint4 bn[3];
+        const uint4* bt = tblk + lane;
+        if (has_tile) {
+            th = hdr[t];
+            bt += th.z;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bn[p] = bt[p * 64];
+        }
+
+        // Phase 1: new M columns → planar LDS ring.  Three register sets
+        // rotate so that each step's gathers have two steps of HSV work to land.
+        const int c0 = ck.c0, ng4 = ck.ng4, nsteps = ck.nsteps;
+        auto process = [&](const Raw4& P, int st) {
+            const int cg = wave * 4 + 16 * st + (lane & 3);
+            const int x = c0 + 4 * cg;
+            const bool active = (cg < ng4) && (r < nrows);
+            uint32_t px[4], zb[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                zb[k] = ~0u;
+                if (ZONES) {
+                    zb[k] = 0;
+#pragma unroll
+                    for (int q = 0; q < NR; ++q) zb[k] |= (uint32_t)((uint32_t)(x + k - zc0[q]) < (uint32_t)zcw[q]) << q;
+                    zb[k] &= zrow;
+                }
+            }
+            // One branch per step (not per pixel) so the four pixels' table
+            // reads and arithmetic interleave in one basic block.
+            uint32_t ch[4];
+            if (__builtin_amdgcn_ballot_w64(P.any) != 0ull) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    uint32_t raw = P.p[k];
+                    if (CLAMP) raw >>= P.sh[k];
+                    px[k] = (DBG & 2) ? (raw | 0x80808080u) : hsv2_px<NR, ZONES>(L, raw, zb[k]);
+                }
+                transpose4(px[0], px[1], px[2], px[3], ch);
+            } else if (ZONES) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) px[k] = hsv2_px<NR, ZONES>(L, 0u, zb[k]);
+                transpose4(px[0], px[1], px[2], px[3], ch);
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) ch[c] = ((fill >> (8 * c)) & 0xFFu) * 0x01010101u;
+            }
+            if (active) {
+                const int pos = x & (RING - 1);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) *reinterpret_cast<uint32_t*>(&L.win[c][r][pos]) = ch[c];
+            }
+        };
+        for (int st = 0; st < nsteps; st += 3) {
+            if (st + 2 < nsteps) issue(ck, st + 2, xxl + (st + 2) * sx, yyl + (st + 2) * sy, xl + 64 * (st + 2), RC);
+            process(RA, st);
+            if (st + 1 >= nsteps) break;
+            if (st + 3 < nsteps) issue(ck, st + 3, xxl + (st + 3) * sx, yyl + (st + 3) * sy, xl + 64 * (st + 3), RA);
+            process(RB, st + 1);
+            if (st + 2 >= nsteps) break;
+            if (st + 4 < nsteps) issue(ck, st + 4, xxl + (st + 4) * sx, yyl + (st + 4) * sy, xl + 64 * (st + 4), RB);
+            process(RC, st + 2);
+        }
+
+        // Next chunk's first two steps: their gathers fly during phase 2.
+        const int s1 = ck.s1;
+        const bool more = s1 < ntiles;
+        if (more) {
+            ck = hp2_chunk(hdr, s1, ntiles, filled, wave);
+            xl = lane_x(ck);
+            xxl = B.rowx + (uint32_t)xl * (uint32_t)B.b0;
+            yyl = B.rowy + (uint32_t)xl * (uint32_t)B.b3;
+            if (ck.nsteps > 0) issue(ck, 0, xxl, yyl, xl, RA);
+            if (ck.nsteps > 1) issue(ck, 1, xxl + sx, yyl + sy, xl + 64, RB);
+        }
+        __syncthreads();
+
+        // Phase 2 (mfma): wave w takes tile s0 + w; A = 16 window rows × 64
+        // columns of one channel (lane l: row l&15, bytes 16(l>>4)..+15),
+        // B = 64 columns × 16 outputs of one tap byte plane.  D lane l =
+        // output l&15, rows 4(l>>4)..+3 = exactly one 16-B T group.
+        if (has_tile) {
+            i32x4 acc[4][3];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) acc[c][p] = i32x4{0, 0, 0, 0};
+            const int arow = lane & 15, akoff = 16 * (lane >> 4);
+#pragma unroll 1
+            for (int ks = 0; ks < th.y; ++ks) {
+                i32x4 bq[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) bq[p] = __builtin_bit_cast(i32x4, bn[p]);
+                if (ks + 1 < th.y) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) bn[p] = bt[((ks + 1) * 3 + p) * 64];
+                }
+                const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const i32x4 a = *reinterpret_cast<const i32x4*>(&L.win[c][arow][pos]);
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        acc[c][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[p], acc[c][p], 0, 0, 0);
+                }
+            }
+            const int xo = 16 * t + (lane & 15);
+            if (xo < h.out_len) {
+                const int32_t bias = tbias[xo];
+                uint32_t outc[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int32_t ss = bias + acc[c][0][rr] + (acc[c][1][rr] << 8) + (acc[c][2][rr] << 16);
+                        outc[c] |= clip8(ss) << (8 * rr);
+                    }
+                const int grp = (row0 >> 2) + (lane >> 4);
+                uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
+                *dst = make_uint4(outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
+                                  outc[3] ^ 0x80808080u);
+            }
+        }
+        if (!more) break;
+        __syncthreads();
+    }
+}
+
+template <int NR, bool ZONES, int CN, int DBG = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
+              const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp) {
+    __shared__ Hpass2Lds<NR> L;
+    typedef typename MaskType<NR>::T MT;
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / tiles_y;
+    const int ty = b - im * tiles_y;
+    const ipp_gather_desc g = descs[im].g;
+    const ipp_resample_desc h = descs[im].h;
+    const int row0 = ty * HR;
+    if (row0 >= h.lines) return;  // block-uniform
+
+    // Tables (one entry per thread, hm: 192 entries).
+    {
+        const int i = threadIdx.x;
+        uint32_t vmk = 0, smk = 0, hmk = 0;
+        int hh = i - 32;
+        hh = hh < 0 ? hh + 180 : hh;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            const ipp_hsv_range& q = hp.r[k];
+            vmk |= (uint32_t)(i >= q.lo[2] && i <= q.hi[2]) << k;
+            smk |= (uint32_t)(i >= q.lo[1] && i <= q.hi[1]) << k;
+            hmk |= (uint32_t)(hh >= q.lo[0] && hh <= q.hi[0]) << k;
+        }
+        L.sv[i] = (uint32_t)kSdiv[i];
+        L.hd[i] = kHdiv180[i];
+        L.vm[i] = (MT)vmk;
+        L.sm[i] = (MT)smk;
+        if (i < HMN) L.hm[i] = (MT)hmk;
+    }
+
+    // Zones: per-lane row bits now, column bits per pixel.
+    int32_t zc0[ZONES ? NR : 1], zcw[ZONES ? NR : 1];
+    uint32_t zrow = 0;
+    const int lane = threadIdx.x & 63;
+    const int y = h.line0 + row0 + (lane >> 2);
+    if (ZONES) {
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            int a, bb, cc, dd;
+            slice_indices(hp.r[k].zone[0], g.out_h - hp.r[k].zone[1], g.out_h, a, bb);
+            slice_indices(hp.r[k].zone[2], g.out_w - hp.r[k].zone[3], g.out_w, cc, dd);
+            zrow |= (uint32_t)(y >= a && y < bb) << k;
+            zc0[k] = cc;
+            zcw[k] = dd - cc;
+        }
+    }
+
+    // Source window as a buffer resource: every in-window dword read is in
+    // range; out-of-window pixels use offset 0xFFFFFFFF (range check → 0).
+    const Sampler S = make_sampler(src, g);
+    // (32-bit scalar arithmetic: a 64-bit min would land in VGPRs and turn every
+    // buffer load into a waterfall loop; items are < 2 GiB, checked on the host.)
+    const int nrec = (g.src_h - g.in_y0) * g.src_pitch - g.in_x0 * g.src_cn;
+    const int need = (g.in_h - 1) * g.src_pitch + g.in_w * CN + (CN == 3 ? 1 : 0);
+    const bool clamp = need > nrec;  // last pixel's dword would cross the image end (block-uniform)
+    const uint64_t sbu = reinterpret_cast<uint64_t>(S.base);
+    Hp2Block B;
+    B.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(sbu), (short)0, nrec, 0x00020000);
+    B.lim = S.lim;
+    B.rowx = (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1;
+    B.rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
+    B.b0 = S.b0;
+    B.b3 = S.b3;
+    B.pitch = (int32_t)S.pitch;
+    B.in_w = S.in_w;
+    B.in_h = S.in_h;
+    {
+        // Row y's valid columns: 0 <= xx(x) < in_w·2^16 and 0 <= yy(x) < in_h·2^16,
+        // both linear in x; ±2 columns of slack absorb the rounding.  Union over
+        // the block's 16 rows (lanes 4r..4r+3 hold row r) by readlane.
+        float lo = -1e9f, hi = 1e9f;
+        auto clip = [&](float a, float bb, float lim) {
+            if (bb == 0.0f) {
+                if (!(a >= 0.0f && a < lim)) { lo = 1e9f; hi = -1e9f; }
+            } else {
+                const float t1 = -a / bb, t2 = (lim - a) / bb;
+                lo = fmaxf(lo, fminf(t1, t2));
+                hi = fminf(hi, fmaxf(t1, t2));
+            }
+        };
+        clip((float)(int32_t)B.rowx, (float)S.b0, 65536.0f * (float)S.in_w);
+        clip((float)(int32_t)B.rowy, (float)S.b3, 65536.0f * (float)S.in_h);
+        int ilo = lo > hi ? 0x3FFFFFFF : (int)fmaxf(lo - 2.0f, -1e8f);
+        int ihi = lo > hi ? -0x3FFFFFFF : (int)fminf(hi + 2.0f, 1e8f);
+        int blo = 0x3FFFFFFF, bhi = -0x3FFFFFFF;
+#pragma unroll
+        for (int rr = 0; rr < HR; ++rr) {
+            blo = min(blo, __builtin_amdgcn_readlane(ilo, 4 * rr));
+            bhi = max(bhi, __builtin_amdgcn_readlane(ihi, 4 * rr));
+        }
+        B.xlo = (DBG & 8) ? -0x3FFFFFFF : blo;
+        B.xhi = (DBG & 8) ? 0x3FFFFFFF : bhi;
+    }
+
+    __syncthreads();  // tables visible
+    // Fill value (raw 0): uniform over the block except for zone bits.
+    const uint32_t fill = hsv2_px<NR, ZONES>(L, 0u, ~0u);
+    const int nrows = min(HR, h.lines - row0);
+    if (CN == 3 && clamp)
+        hpass2_body<NR, ZONES, CN, true, DBG>(L, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+    else
+        hpass2_body<NR, ZONES, CN, false, DBG>(L, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+}
+
 // V pass over T (dot4) → unpremultiply → blend onto the background, fused with
 // the background copy.  Block = VR composite rows.
 template <int STORE>
@@ -497,7 +892,27 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
         const char* e = getenv("IPP_DBG_HPASS");  // diagnostics (wrong output): 1 no HSV, 2 no H taps, 3 neither
         return e ? atoi(e) : 0;
     }();
-    if (fmt == IPP_TAPS_MFMA && dbg == 1)
+    static const int impl = [] {
+        const char* e = getenv("IPP_HPASS");  // 1: previous (packed-compare HSV) kernel
+        return e ? atoi(e) : 2;
+    }();
+    if (fmt == IPP_TAPS_MFMA && dbg == 0 && impl == 2)
+        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
+    else if (fmt == IPP_TAPS_MFMA && impl == 2 && dbg >= 10 && (NR == 4 && !ZONES && CN == 3)) {
+        // diagnostics (wrong output): 10+d, d bit0 coalesced gathers, bit1 no HSV, bit2 no phase 2;
+        // 18: no fill-step skipping (correct output)
+        switch (dbg - 10) {
+            case 1: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
+            case 2: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 2>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
+            case 3: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 3>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
+            case 4: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 4>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
+            case 5: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 5>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
+            case 6: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 6>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
+            case 7: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 7>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
+            default: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 8>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
+        }
+    }
+    else if (fmt == IPP_TAPS_MFMA && dbg == 1)
         hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
     else if (fmt == IPP_TAPS_MFMA && dbg == 2)
         hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 2>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
