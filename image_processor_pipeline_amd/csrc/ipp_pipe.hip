@@ -373,6 +373,7 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
             off = offc;
         }
         if (DBG & 1) off = (uint32_t)((x >> 6) * 768 + (threadIdx.x & 63) * 3 + k * 192 + (threadIdx.x >> 8) * 3072);
+        if (DBG & 16) off &= 0x7FFFu;  // same scatter, 32 KiB footprint (cache-resident)
         off = ok ? off : 0xFFFFFFFFu;
         o.p[k] = __builtin_amdgcn_raw_buffer_load_b32(B.rs, off, 0, 0);
         any |= ok;
@@ -909,6 +910,8 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
             case 5: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 5>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
             case 6: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 6>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
             case 7: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 7>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
+            case 16: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 16>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
+            case 20: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 20>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
             default: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 8>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
         }
     }
