@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=192)
+    ap.add_argument("--unsplit", action="store_true", help="pipe5: ipp_pipe_hpass + full-frame ipp_pipe_vblend")
     return ap.parse_args()
 
 
@@ -130,8 +131,16 @@ def main():
         plan = fused.plan_pipe((S, S), B, (S, S), K, cfg, seed=args.seed * 7919, item_range=(start, stop))
         runner = fused.PipeRunner(plan, dev)
         out = torch.empty((B, S, S, 3), dtype=torch.uint8, device=dev)
-        algo = {"ipp_pipe_hpass": plan.algo_bytes_hpass, "ipp_pipe_vblend": plan.algo_bytes_vblend}
-        launches = [("ipp_pipe_hpass", lambda: runner.hpass(src)), ("ipp_pipe_vblend", lambda: runner.vblend(bgs, out))]
+        if runner.split and not args.unsplit:
+            # the H pass also copies the background rows outside the overlay bands
+            algo = {"ipp_pipe_hpass_bgcopy": plan.algo_bytes_hpass_bgcopy,
+                    "ipp_pipe_vblend_bands": plan.algo_bytes_vblend_bands}
+            launches = [("ipp_pipe_hpass_bgcopy", lambda: runner.hpass_bgcopy(src, bgs, out)),
+                        ("ipp_pipe_vblend_bands", lambda: runner.vblend_bands(bgs, out))]
+        else:
+            algo = {"ipp_pipe_hpass": plan.algo_bytes_hpass, "ipp_pipe_vblend": plan.algo_bytes_vblend}
+            launches = [("ipp_pipe_hpass", lambda: runner.hpass(src)),
+                        ("ipp_pipe_vblend", lambda: runner.vblend(bgs, out))]
         workload = "5-stage pipe: crop(64px)->rotate(NEAREST,expand,bbox)->flip->HSV mask(4 ref ranges)->LANCZOS+paste"
     elif args.workload == "video4k":
         from image_processor_pipeline_amd import video_chain

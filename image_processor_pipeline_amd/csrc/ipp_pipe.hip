@@ -21,6 +21,8 @@
 // T (H-pass output) layout per item: [row group g][column x'][4 channels][4
 // rows] bytes (16 B per (g, x')), values XOR 0x80, so the V pass reads one
 // dwordx4 per 4 taps per pixel.  T rows are M rows [line0, line0 + lines).
+#include <algorithm>
+
 #include "ipp_hsv.h"
 #include "ipp_sampler.h"
 
@@ -580,10 +582,72 @@ __device__ __forceinline__ void hpass2_body(Hpass2Lds<NR>& L, const Hp2Block& B,
     }
 }
 
-template <int NR, bool ZONES, int CN, int DBG = 0>
+// Composite rows outside the overlay's 16-row bands [vb0, vb1) are plain
+// copies of the background (Paste.c leaves them untouched).  The H-pass
+// blocks of an item share that copy (block `share` of `nshare`): it rides on a
+// memory system the VALU-bound H pass leaves idle, and ipp_pipe_vblend_bands
+// then only visits the bands the overlay touches.
+__device__ __forceinline__ void paste_bands(const ipp_paste_desc& p, int& vb0, int& vb1) {
+    vb0 = (p.y >> 4) << 4;
+    vb1 = min(p.bg_h, ((p.y + p.ov_h + 15) >> 4) << 4);
+    vb1 = max(vb1, vb0);
+}
+
+__device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, const uint8_t* __restrict__ bg,
+                                                      uint8_t* __restrict__ dst, int share, int nshare) {
+    int vb0, vb1;
+    paste_bands(p, vb0, vb1);
+    const int rb = 3 * p.bg_w;
+    const uint8_t* sb = bg + p.bg_off;
+    uint8_t* db = dst + p.dst_off;
+    const bool flat = p.bg_pitch == rb && p.dst_pitch == rb && (rb & 15) == 0 &&
+                      ((reinterpret_cast<uintptr_t>(sb) | reinterpret_cast<uintptr_t>(db)) & 15u) == 0;
+    if (flat) {
+        // Two flat byte ranges [0, vb0·rb) and [vb1·rb, bg_h·rb) in 16-B vectors.
+        const int64_t n0 = (int64_t)vb0 * rb / 16, n1 = (int64_t)(p.bg_h - vb1) * rb / 16, V = n0 + n1;
+        const int64_t a = V * share / nshare, e = V * (share + 1) / nshare;
+        const int64_t skip = (int64_t)vb1 * rb / 16 - n0;  // vector index gap over the bands
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(sb);
+        u32x4* d4 = reinterpret_cast<u32x4*>(db);
+        for (int64_t i0 = a + threadIdx.x; i0 < e; i0 += 8 * 256) {
+            u32x4 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int64_t i = i0 + 256 * j;
+                if (i < e) v[j] = s4[i < n0 ? i : i + skip];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int64_t i = i0 + 256 * j;
+                if (i < e) __builtin_nontemporal_store(v[j], d4 + (i < n0 ? i : i + skip));
+            }
+        }
+        return;
+    }
+    // General pitches: whole rows, 16-B chunks with byte tails.
+    const int R = vb0 + (p.bg_h - vb1);
+    const int ra = (int)((int64_t)R * share / nshare), re = (int)((int64_t)R * (share + 1) / nshare);
+    const int chunks = (rb + 15) >> 4;
+    for (int rr = ra; rr < re; ++rr) {
+        const int y = rr < vb0 ? rr : rr - vb0 + vb1;
+        const uint8_t* brow = sb + (int64_t)y * p.bg_pitch;
+        uint8_t* drow = db + (int64_t)y * p.dst_pitch;
+        for (int ci = threadIdx.x; ci < chunks; ci += 256) {
+            const int c0 = ci << 4, nb = min(16, rb - c0);
+            const bool vec = nb == 16 && ((reinterpret_cast<uintptr_t>(brow + c0) | reinterpret_cast<uintptr_t>(drow + c0)) & 15u) == 0;
+            uint32_t w[4];
+            load16(brow + c0, nb, vec, w);
+            store16<2>(drow + c0, nb, vec, w);
+        }
+    }
+}
+
+template <int NR, bool ZONES, int CN, int DBG = 0, bool COPY = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
-              const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp) {
+              const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp, const uint8_t* __restrict__ bg,
+              uint8_t* __restrict__ dst) {
     __shared__ Hpass2Lds<NR> L;
     typedef typename MaskType<NR>::T MT;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
@@ -686,6 +750,9 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
         hpass2_body<NR, ZONES, CN, true, DBG>(L, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
     else
         hpass2_body<NR, ZONES, CN, false, DBG>(L, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+    // Last, so that no gather of this block waits behind the copy's stores
+    // (stores count in vmcnt on gfx9).
+    if (COPY) bg_copy_outside_bands(descs[im].p, bg, dst, ty, (h.lines + HR - 1) / HR);
 }
 
 // V pass over T (dot4) → unpremultiply → blend onto the background, fused with
@@ -773,7 +840,7 @@ k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, u
 // per lane give all four channels), D lane l = column l&15, rows 4(l>>4)..+3.
 constexpr int VBR = 16;
 
-template <int STORE, int DBG = 0>
+template <int STORE, int DBG = 0, bool BANDS = false>
 __global__ void __launch_bounds__(256)
 k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
                    const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int tiles_y,
@@ -783,7 +850,13 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
     const int im = b / tiles_y;
     const int ty = b - im * tiles_y;
     const ipp_paste_desc p = descs[im].p;
-    const int y0 = ty * VBR;
+    int y0 = ty * VBR;
+    if (BANDS) {  // only the 16-row bands the overlay touches (the rest: ipp_pipe_hpass_bgcopy)
+        int vb0, vb1;
+        paste_bands(p, vb0, vb1);
+        y0 += vb0;
+        if (y0 >= vb1) return;
+    }
     if (y0 >= p.bg_h) return;
     const int nrows = min(VBR, p.bg_h - y0);
     const int oy_lo = max(0, y0 - p.y), oy_hi = min(p.ov_h, y0 + nrows - p.y);
@@ -888,7 +961,8 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
 
 template <int NR, bool ZONES, int CN>
 void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
-                  const ipp_pipe_desc* descs, int fmt, int ty, const ipp_hsv_params& hp) {
+                  const ipp_pipe_desc* descs, int fmt, int ty, const ipp_hsv_params& hp, const uint8_t* bg,
+                  uint8_t* dst) {
     static const int dbg = [] {
         const char* e = getenv("IPP_DBG_HPASS");  // diagnostics (wrong output): 1 no HSV, 2 no H taps, 3 neither
         return e ? atoi(e) : 0;
@@ -897,22 +971,25 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
         const char* e = getenv("IPP_HPASS");  // 1: previous (packed-compare HSV) kernel
         return e ? atoi(e) : 2;
     }();
-    if (fmt == IPP_TAPS_MFMA && dbg == 0 && impl == 2)
-        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
+    if (bg && dst) {  // H pass + the background rows outside the overlay bands
+        if (fmt != IPP_TAPS_MFMA) return;  // rejected by the entry point
+        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 0, true>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst);
+    } else if (fmt == IPP_TAPS_MFMA && dbg == 0 && impl == 2)
+        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst);
     else if (fmt == IPP_TAPS_MFMA && impl == 2 && dbg >= 10 && (NR == 4 && !ZONES && CN == 3)) {
         // diagnostics (wrong output): 10+d, d bit0 coalesced gathers, bit1 no HSV, bit2 no phase 2;
         // 18: no fill-step skipping (correct output)
         switch (dbg - 10) {
-            case 1: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
-            case 2: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 2>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
-            case 3: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 3>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
-            case 4: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 4>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
-            case 5: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 5>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
-            case 6: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 6>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
-            case 7: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 7>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
-            case 16: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 16>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
-            case 20: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 20>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
-            default: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 8>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp); break;
+            case 1: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
+            case 2: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 2>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
+            case 3: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 3>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
+            case 4: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 4>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
+            case 5: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 5>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
+            case 6: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 6>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
+            case 7: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 7>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
+            case 16: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 16>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
+            case 20: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 20>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
+            default: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 8>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
         }
     }
     else if (fmt == IPP_TAPS_MFMA && dbg == 1)
@@ -933,13 +1010,14 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
 
 template <int NR>
 void launch_hpass_nr(bool zones, int cn, dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp,
-                     const int32_t* coefs, const ipp_pipe_desc* descs, int fmt, int ty, const ipp_hsv_params& hp) {
+                     const int32_t* coefs, const ipp_pipe_desc* descs, int fmt, int ty, const ipp_hsv_params& hp,
+                     const uint8_t* bg, uint8_t* dst) {
     if (zones) {
-        if (cn == 4) launch_hpass<NR, true, 4>(grid, s, src, tmp, coefs, descs, fmt, ty, hp);
-        else launch_hpass<NR, true, 3>(grid, s, src, tmp, coefs, descs, fmt, ty, hp);
+        if (cn == 4) launch_hpass<NR, true, 4>(grid, s, src, tmp, coefs, descs, fmt, ty, hp, bg, dst);
+        else launch_hpass<NR, true, 3>(grid, s, src, tmp, coefs, descs, fmt, ty, hp, bg, dst);
     } else {
-        if (cn == 4) launch_hpass<NR, false, 4>(grid, s, src, tmp, coefs, descs, fmt, ty, hp);
-        else launch_hpass<NR, false, 3>(grid, s, src, tmp, coefs, descs, fmt, ty, hp);
+        if (cn == 4) launch_hpass<NR, false, 4>(grid, s, src, tmp, coefs, descs, fmt, ty, hp, bg, dst);
+        else launch_hpass<NR, false, 3>(grid, s, src, tmp, coefs, descs, fmt, ty, hp, bg, dst);
     }
 }
 
@@ -953,9 +1031,10 @@ extern "C" int ipp_dbg_dump(void* win, void* meta) {
 }
 #endif
 
-extern "C" int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
-                              int32_t n_images, int32_t max_out_w, int32_t max_rows, int32_t src_cn,
-                              const ipp_hsv_params* hsv, int32_t tap_format, void* stream) {
+static int pipe_hpass_impl(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
+                           int32_t n_images, int32_t max_out_w, int32_t max_rows, int32_t src_cn,
+                           const ipp_hsv_params* hsv, int32_t tap_format, const uint8_t* bg, uint8_t* dst,
+                           void* stream) {
     if (n_images == 0) return IPP_OK;
     if (!src || !tmp || !coefs || !descs || !hsv || n_images < 0 || max_out_w <= 0 || max_rows <= 0) return IPP_E_ARG;
     if (src_cn != 3 && src_cn != 4) return IPP_E_ARG;
@@ -974,24 +1053,59 @@ extern "C" int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* c
     // A range that never matches: lo_v = 1 > hi_v = 0 (cv::inRange's empty range).
     const ipp_hsv_range never = ipp_hsv_range{{0, 0, 1}, {180, 255, 0}, {0, 0, 0, 0}};
     switch (hsv->n_ranges) {
-        case 1: launch_hpass_nr<1>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv); break;
-        case 2: launch_hpass_nr<2>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv); break;
-        case 3: launch_hpass_nr<3>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv); break;
-        case 4: launch_hpass_nr<4>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv); break;
+        case 1: launch_hpass_nr<1>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv, bg, dst); break;
+        case 2: launch_hpass_nr<2>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv, bg, dst); break;
+        case 3: launch_hpass_nr<3>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv, bg, dst); break;
+        case 4: launch_hpass_nr<4>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv, bg, dst); break;
         case 5: case 6: {
             ipp_hsv_params q = *hsv;  // pad with never-matching ranges (lo > hi in v)
             for (int k = q.n_ranges; k < 6; ++k) q.r[k] = never;
-            launch_hpass_nr<6>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, q);
+            launch_hpass_nr<6>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, q, bg, dst);
             break;
         }
         default: {
             if (hsv->n_ranges > IPP_MAX_HSV_RANGES) return IPP_E_ARG;
             ipp_hsv_params q = *hsv;
             for (int k = q.n_ranges; k < IPP_MAX_HSV_RANGES; ++k) q.r[k] = never;
-            launch_hpass_nr<IPP_MAX_HSV_RANGES>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, q);
+            launch_hpass_nr<IPP_MAX_HSV_RANGES>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, q, bg, dst);
             break;
         }
     }
+    IPP_CHECK_LAUNCH();
+    return IPP_OK;
+}
+
+extern "C" int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
+                              int32_t n_images, int32_t max_out_w, int32_t max_rows, int32_t src_cn,
+                              const ipp_hsv_params* hsv, int32_t tap_format, void* stream) {
+    return pipe_hpass_impl(src, tmp, coefs, descs, n_images, max_out_w, max_rows, src_cn, hsv, tap_format, nullptr,
+                           nullptr, stream);
+}
+
+extern "C" int ipp_pipe_hpass_bgcopy(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
+                                     const ipp_pipe_desc* descs, int32_t n_images, int32_t max_out_w,
+                                     int32_t max_rows, int32_t src_cn, const ipp_hsv_params* hsv,
+                                     int32_t tap_format, const uint8_t* bg, uint8_t* dst, void* stream) {
+    if (n_images == 0) return IPP_OK;
+    if (!bg || !dst || tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;
+    return pipe_hpass_impl(src, tmp, coefs, descs, n_images, max_out_w, max_rows, src_cn, hsv, tap_format, bg, dst,
+                           stream);
+}
+
+extern "C" int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst, const int32_t* coefs,
+                                     const ipp_pipe_desc* descs, int32_t n_images, int32_t bg_w, int32_t bg_h,
+                                     int32_t max_ov_w, int32_t max_ov_h, int32_t tap_format, void* stream) {
+    if (n_images == 0) return IPP_OK;
+    if (!tmp || !bg || !dst || !coefs || !descs || n_images < 0 || bg_w <= 0 || bg_h <= 0) return IPP_E_ARG;
+    if (tap_format != IPP_TAPS_MFMA || max_ov_w <= 0 || max_ov_w > bg_w || max_ov_h <= 0 || max_ov_h > bg_h)
+        return IPP_E_ARG;
+    const size_t sm = (size_t)VBR * max_ov_w * sizeof(uint32_t);
+    // an overlay of height H at any y spans at most ceil((15 + H) / 16) bands
+    const int tyb = std::min((max_ov_h + 15 + VBR - 1) / VBR, (bg_h + VBR - 1) / VBR);
+    const int64_t nb = (int64_t)tyb * n_images;
+    if (nb >= INT32_MAX || sm > 64 * 1024) return IPP_E_ARG;
+    hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 0, true>), dim3((uint32_t)nb), dim3(256), sm, (hipStream_t)stream, tmp,
+                       bg, dst, coefs, descs, tyb, max_ov_w);
     IPP_CHECK_LAUNCH();
     return IPP_OK;
 }

@@ -75,6 +75,11 @@ class PipePlan:
     algo_bytes_vblend: int = 0
     tap_format: int = 0                   # IPP_TAPS_DOT4 / IPP_TAPS_MFMA (H and V passes)
     max_ov_w: int = 1
+    max_ov_h: int = 1
+    # split form (ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands): the
+    # background rows outside the overlay bands move with the H pass
+    algo_bytes_hpass_bgcopy: int = 0
+    algo_bytes_vblend_bands: int = 0
 
 
 def draw_params(n: int, src_hw: Tuple[int, int], bg_hw: Tuple[int, int], n_bg: int, cfg: PipeConfig,
@@ -190,7 +195,7 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     # ---- descriptors ----------------------------------------------------
     tmp_off = 0
     max_out_w = max_rows = 1
-    algo_h = algo_v = 0
+    algo_h = algo_v = copy_rows = 0
     for i in range(n):
         rh, rw = cut_dims[i]
         nh_, nw_ = ov_dims[i]
@@ -229,6 +234,9 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
         t_bytes = pitch * ((rows + 3) // 4)
         algo_h += 3 * hc * wc + t_bytes
         algo_v += t_bytes + 3 * bh * bw + 3 * bh * bw
+        vb0 = (it.y // 16) * 16                      # overlay bands (ipp.h, ipp_pipe_vblend_bands)
+        vb1 = max(vb0, min(bh, -(-(it.y + nh_) // 16) * 16))
+        copy_rows += bh - (vb1 - vb0)
     # Processing order: group items by background so that the items pasting
     # onto one background run back to back (and, through the XCD-aware block
     # mapping, on one XCD): the 3 MB background then stays in L2/L3 instead of
@@ -236,9 +244,11 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     order = np.argsort(np.array([it.bg_index for it in params]), kind="stable")
     d = d[order]
     hsv = G.hsv_params(cfg.hsv_ranges, cfg.zones, cfg.use_gimp_scale, bgr=False)
+    copy_bytes = 2 * 3 * bw * copy_rows           # read + write of the rows outside the bands
     return PipePlan(d, coefs, hsv, params, cut_dims, ov_dims, max(tmp_off, 256), max_out_w, max_rows, bw, bh,
                     algo_h, algo_v, N.IPP_TAPS_MFMA if mfma else N.IPP_TAPS_DOT4,
-                    max(w for _, w in ov_dims))
+                    max(w for _, w in ov_dims), max(h for h, _ in ov_dims),
+                    algo_h + copy_bytes, algo_v - copy_bytes)
 
 
 class PipeRunner:
@@ -264,10 +274,34 @@ class PipeRunner:
                                          self.descs.data_ptr(), len(p.descs), p.bg_w, p.bg_h, p.max_ov_w,
                                          p.tap_format, _stream(self.device)), "ipp_pipe_vblend")
 
+    def hpass_bgcopy(self, src: torch.Tensor, bgs: torch.Tensor, out: torch.Tensor) -> None:
+        """H pass + the composite rows outside the overlay bands (split form)."""
+        p = self.plan
+        N.check(self.lib.ipp_pipe_hpass_bgcopy(src.data_ptr(), self.tmp.data_ptr(), self.coefs.data_ptr(),
+                                               self.descs.data_ptr(), len(p.descs), p.max_out_w, p.max_rows, 3,
+                                               N.np_ptr(p.hsv), p.tap_format, bgs.data_ptr(), out.data_ptr(),
+                                               _stream(self.device)), "ipp_pipe_hpass_bgcopy")
+
+    def vblend_bands(self, bgs: torch.Tensor, out: torch.Tensor) -> None:
+        """V pass + paste over the 16-row bands the overlay touches (split form)."""
+        p = self.plan
+        N.check(self.lib.ipp_pipe_vblend_bands(self.tmp.data_ptr(), bgs.data_ptr(), out.data_ptr(),
+                                               self.coefs.data_ptr(), self.descs.data_ptr(), len(p.descs), p.bg_w,
+                                               p.bg_h, p.max_ov_w, p.max_ov_h, p.tap_format,
+                                               _stream(self.device)), "ipp_pipe_vblend_bands")
+
+    @property
+    def split(self) -> bool:
+        return self.plan.tap_format == N.IPP_TAPS_MFMA
+
     def run(self, src: torch.Tensor, bgs: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         for t, name in ((src, "src"), (bgs, "bgs"), (out, "out")):
             if not (t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous()):
                 raise N.NativeUnavailable(f"PipeRunner.run: {name} must be a contiguous uint8 ROCm tensor")
-        self.hpass(src)
-        self.vblend(bgs, out)
+        if self.split:
+            self.hpass_bgcopy(src, bgs, out)
+            self.vblend_bands(bgs, out)
+        else:
+            self.hpass(src)
+            self.vblend(bgs, out)
         return out

@@ -201,6 +201,26 @@ int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
                     int32_t bg_w, int32_t bg_h, int32_t max_ov_w, int32_t tap_format,
                     void* stream);
 
+/* Split form of the pair above (MFMA taps only), used by the batched device
+ * mode (fused.PipeRunner.run).  A composite's rows outside the 16-row bands
+ * the overlay touches, [16⌊y/16⌋, 16⌈(y + ov_h)/16⌉), are plain copies of the
+ * background (Paste.c, overlays.py:138-139, leaves them untouched):
+ *   ipp_pipe_hpass_bgcopy = ipp_pipe_hpass + the copy of those rows, spread
+ *     over the H-pass blocks of the item (the H pass is VALU-bound and leaves
+ *     the memory system idle);
+ *   ipp_pipe_vblend_bands = ipp_pipe_vblend restricted to the overlay bands;
+ *     max_ov_h bounds the overlay heights.
+ * Together they write exactly what ipp_pipe_hpass + ipp_pipe_vblend write. */
+int ipp_pipe_hpass_bgcopy(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
+                          const ipp_pipe_desc* descs, int32_t n_images,
+                          int32_t max_out_w, int32_t max_rows, int32_t src_cn,
+                          const ipp_hsv_params* hsv, int32_t tap_format,
+                          const uint8_t* bg, uint8_t* dst, void* stream);
+int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
+                          const int32_t* coefs, const ipp_pipe_desc* descs, int32_t n_images,
+                          int32_t bg_w, int32_t bg_h, int32_t max_ov_w, int32_t max_ov_h,
+                          int32_t tap_format, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* K10-K13: pixels_isolés.keep_largest_component                             */
 /* :32 threshold(α,1,255) :35 connectedComponentsWithStats(8) :38-55 keep    */

@@ -239,6 +239,33 @@ def test_pipe_structured_content_vs_oracle(D):
         assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), i
 
 
+def test_pipe_split_equals_unsplit(D):
+    """ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands write exactly what
+    ipp_pipe_hpass + ipp_pipe_vblend write; odd background widths take the
+    row-wise copy path (3·bw not a multiple of 16)."""
+    from image_processor_pipeline_amd import fused
+    cfg = fused.PipeConfig(margins=(3, 5, 2, 7), scale_min=0.2, scale_max=0.6)
+    for (bh, bw) in [(97, 125), (64, 96)]:
+        n, H, W = 8, 90, 110
+        rng = np.random.default_rng(bw)
+        src = rng.integers(0, 256, (n, H, W, 3), np.uint8)
+        bgs = rng.integers(0, 256, (3, bh, bw, 3), np.uint8)
+        plan = fused.plan_pipe((H, W), n, (bh, bw), 3, cfg, seed=bw)
+        runner = fused.PipeRunner(plan, DEV)
+        assert runner.split
+        a = torch.full((n, bh, bw, 3), 7, dtype=torch.uint8, device=DEV)
+        b = torch.full((n, bh, bw, 3), 9, dtype=torch.uint8, device=DEV)
+        runner.hpass_bgcopy(_t(src), _t(bgs), a)
+        runner.vblend_bands(_t(bgs), a)
+        runner.hpass(_t(src))
+        runner.vblend(_t(bgs), b)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+        got = a.cpu().numpy()
+        for i in range(n):
+            assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (bw, i)
+
+
 def test_pipe_fullsize_items_vs_oracle(D):
     """BASELINE config 3 geometry (1024² sources, 64-px margins, 1024² bgs)."""
     from image_processor_pipeline_amd import fused
