@@ -33,6 +33,7 @@ constexpr int HR = 16;            // H-pass rows per block (4 per thread)
 constexpr int RING = 512;         // window ring: M columns x live at x & (RING - 1)
 constexpr int WSTRIDE = 528;      // LDS bytes per plane row (≡ 4 dwords mod 32 banks)
 constexpr int VR = 4;             // composite rows per vblend block
+constexpr int kCopyBlocksPerItem = 12;  // ipp_pipe_hpass_bgcopy: background-copy blocks per item
 
 __device__ __forceinline__ int32_t sdot4(uint32_t a, uint32_t b, int32_t c) {
 #ifdef IPP_DBG_NO_DOT4
@@ -647,12 +648,19 @@ template <int NR, bool ZONES, int CN, int DBG = 0, bool COPY = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
               const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp, const uint8_t* __restrict__ bg,
-              uint8_t* __restrict__ dst) {
+              uint8_t* __restrict__ dst, int cpi) {
     __shared__ Hpass2Lds<NR> L;
     typedef typename MaskType<NR>::T MT;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / tiles_y;
-    const int ty = b - im * tiles_y;
+    // COPY: each item owns tiles_y H-pass blocks followed by cpi background-copy
+    // blocks, so copies run beside the VALU-bound H pass on every XCD.
+    const int per_item = tiles_y + (COPY ? cpi : 0);
+    const int im = b / per_item;
+    const int ty = b - im * per_item;
+    if (COPY && ty >= tiles_y) {
+        bg_copy_outside_bands(descs[im].p, bg, dst, ty - tiles_y, cpi);
+        return;
+    }
     const ipp_gather_desc g = descs[im].g;
     const ipp_resample_desc h = descs[im].h;
     const int row0 = ty * HR;
@@ -750,9 +758,7 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
         hpass2_body<NR, ZONES, CN, true, DBG>(L, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
     else
         hpass2_body<NR, ZONES, CN, false, DBG>(L, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
-    // Last, so that no gather of this block waits behind the copy's stores
-    // (stores count in vmcnt on gfx9).
-    if (COPY) bg_copy_outside_bands(descs[im].p, bg, dst, ty, (h.lines + HR - 1) / HR);
+
 }
 
 // V pass over T (dot4) → unpremultiply → blend onto the background, fused with
@@ -973,23 +979,25 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
     }();
     if (bg && dst) {  // H pass + the background rows outside the overlay bands
         if (fmt != IPP_TAPS_MFMA) return;  // rejected by the entry point
-        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 0, true>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst);
+        const dim3 g2((uint32_t)(grid.x / ty * (ty + kCopyBlocksPerItem)));
+        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 0, true>), g2, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg,
+                           dst, kCopyBlocksPerItem);
     } else if (fmt == IPP_TAPS_MFMA && dbg == 0 && impl == 2)
-        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst);
+        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0);
     else if (fmt == IPP_TAPS_MFMA && impl == 2 && dbg >= 10 && (NR == 4 && !ZONES && CN == 3)) {
         // diagnostics (wrong output): 10+d, d bit0 coalesced gathers, bit1 no HSV, bit2 no phase 2;
         // 18: no fill-step skipping (correct output)
         switch (dbg - 10) {
-            case 1: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
-            case 2: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 2>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
-            case 3: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 3>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
-            case 4: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 4>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
-            case 5: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 5>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
-            case 6: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 6>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
-            case 7: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 7>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
-            case 16: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 16>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
-            case 20: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 20>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
-            default: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 8>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst); break;
+            case 1: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
+            case 2: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 2>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
+            case 3: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 3>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
+            case 4: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 4>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
+            case 5: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 5>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
+            case 6: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 6>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
+            case 7: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 7>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
+            case 16: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 16>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
+            case 20: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 20>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
+            default: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 8>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
         }
     }
     else if (fmt == IPP_TAPS_MFMA && dbg == 1)
@@ -1041,7 +1049,7 @@ static int pipe_hpass_impl(const uint8_t* src, uint8_t* tmp, const int32_t* coef
     if (tap_format != IPP_TAPS_DOT4 && tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;
     const int fmt = tap_format, ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
     const int64_t blocks = (int64_t)ty * n_images;
-    if (blocks >= INT32_MAX) return IPP_E_ARG;
+    if ((int64_t)(ty + (bg ? kCopyBlocksPerItem : 0)) * n_images >= INT32_MAX) return IPP_E_ARG;
     const dim3 grid((uint32_t)blocks);
     hipStream_t s = (hipStream_t)stream;
     // Zones are needed unless every range's zone is the whole image (all
