@@ -17,10 +17,13 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {  # C-ABI entry point → device kernel symbol
-    "ipp_pipe_hpass": "k_pipe_hpass",
-    "ipp_pipe_vblend": "k_pipe_vblend",
-    "ipp_rotate_flip_nearest": "k_rotate_flip_nearest",
+KERNELS = {  # C-ABI entry point → predicate on the (demangled) device kernel name
+    "ipp_pipe_hpass_bgcopy": lambda k: "k_pipe_hpass2<" in k and ", true>" in k,
+    "ipp_pipe_vblend_bands": lambda k: "k_pipe_vblend_mfma<" in k and ", true>" in k,
+    "ipp_pipe_hpass": lambda k: "k_pipe_hpass" in k and ", true>" not in k,
+    "ipp_pipe_vblend": lambda k: "k_pipe_vblend" in k and ", true>" not in k,
+    "ipp_rotate_flip_nearest": lambda k: "k_rotate_flip_nearest" in k,
+    "ipp_video_keep_largest": lambda k: "k_ccl" in k or "k_video" in k,
 }
 
 
@@ -41,8 +44,8 @@ def main():
     write = per_dispatch(os.path.join(prof, "write"), "WRITE_SIZE")
     res = {"_batch": batch}
     for api, sym in KERNELS.items():
-        fk = [k for k in fetch if sym in k]
-        wk = [k for k in write if sym in k]
+        fk = [k for k in fetch if sym(k)]
+        wk = [k for k in write if sym(k)]
         if not fk or not wk:
             continue
         fv = [v for k in fk for v in fetch[k].values()]
