@@ -33,7 +33,15 @@ constexpr int HR = 16;            // H-pass rows per block (4 per thread)
 constexpr int RING = 512;         // window ring: M columns x live at x & (RING - 1)
 constexpr int WSTRIDE = 528;      // LDS bytes per plane row (≡ 4 dwords mod 32 banks)
 constexpr int VR = 4;             // composite rows per vblend block
-constexpr int kCopyBlocksPerItem = 12;  // ipp_pipe_hpass_bgcopy: background-copy blocks per item
+// ipp_pipe_hpass_bgcopy: background-copy blocks per item (IPP_COPY_BLOCKS overrides)
+inline int copy_blocks_per_item() {
+    static const int v = [] {
+        const char* e = getenv("IPP_COPY_BLOCKS");
+        const int k = e ? atoi(e) : 4;
+        return k < 1 ? 1 : (k > 64 ? 64 : k);
+    }();
+    return v;
+}
 
 __device__ __forceinline__ int32_t sdot4(uint32_t a, uint32_t b, int32_t c) {
 #ifdef IPP_DBG_NO_DOT4
@@ -979,9 +987,9 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
     }();
     if (bg && dst) {  // H pass + the background rows outside the overlay bands
         if (fmt != IPP_TAPS_MFMA) return;  // rejected by the entry point
-        const dim3 g2((uint32_t)(grid.x / ty * (ty + kCopyBlocksPerItem)));
+        const dim3 g2((uint32_t)(grid.x / ty * (ty + copy_blocks_per_item())));
         hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 0, true>), g2, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg,
-                           dst, kCopyBlocksPerItem);
+                           dst, copy_blocks_per_item());
     } else if (fmt == IPP_TAPS_MFMA && dbg == 0 && impl == 2)
         hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0);
     else if (fmt == IPP_TAPS_MFMA && impl == 2 && dbg >= 10 && (NR == 4 && !ZONES && CN == 3)) {
@@ -1049,7 +1057,7 @@ static int pipe_hpass_impl(const uint8_t* src, uint8_t* tmp, const int32_t* coef
     if (tap_format != IPP_TAPS_DOT4 && tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;
     const int fmt = tap_format, ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
     const int64_t blocks = (int64_t)ty * n_images;
-    if ((int64_t)(ty + (bg ? kCopyBlocksPerItem : 0)) * n_images >= INT32_MAX) return IPP_E_ARG;
+    if ((int64_t)(ty + (bg ? copy_blocks_per_item() : 0)) * n_images >= INT32_MAX) return IPP_E_ARG;
     const dim3 grid((uint32_t)blocks);
     hipStream_t s = (hipStream_t)stream;
     // Zones are needed unless every range's zone is the whole image (all
