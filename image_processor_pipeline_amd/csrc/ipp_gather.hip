@@ -23,68 +23,102 @@ struct TileGrid {
     int tiles_x, tiles_y;
 };
 
-// One 64×16 output tile per block, branch-free gathers.  Two lane maps:
+// One column of RT 64×16 output tiles per block (64 × 16·RT pixels),
+// branch-free gathers, all RT tiles' loads issued before the first is used
+// (RT gathers in flight per thread).  Two lane maps:
 //   PATCH: wave w gathers the 16×16 patch at columns 16w.. (lane: row lane>>2,
 //          4 pixels at 4·(lane&3)) — each load instruction's addresses fall in
-//          a compact source patch — then the tile is restaged through LDS so
+//          a compact source patch — then each tile is restaged through LDS so
 //          every wave stores 4 full rows (256 B per row per instruction);
 //   ROWS:  wave w covers rows 4w..4w+3 directly (16 lanes × 4 pixels per row).
-template <int CN, bool PATCH>
-__device__ __forceinline__ void rotate_tile(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                            const ipp_gather_desc& d, int tx, int ty, uint4* stage) {
+constexpr int RT = 4;  // tiles per block (rows of 16)
+
+template <int CN, bool PATCH, bool DENSE = false>
+__device__ __forceinline__ void rotate_tiles(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                             const ipp_gather_desc& d, int tx, int tyb, uint4* stage) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int gy, gx;  // gathered pixel block (row, first column) of this thread
-    if (PATCH) {
+    int gy, gx;  // gathered pixel block (row, first column) of this thread within a tile
+    if (DENSE) {  // pixels (gy, gx), (gy, gx + 8), (gy + 8, gx), (gy + 8, gx + 8)
+        gy = lane >> 3;
+        gx = 16 * wave + (lane & 7);
+    } else if (PATCH) {
         gy = lane >> 2;
         gx = 16 * wave + 4 * (lane & 3);
     } else {
         gy = (int)(threadIdx.x >> 4);
         gx = 4 * (int)(threadIdx.x & 15);
     }
-    if (ty * TILE_H >= d.out_h || tx * TILE_W >= d.out_w) return;  // block-uniform
+    const int ty0 = tyb * RT;
+    if (ty0 * TILE_H >= d.out_h || tx * TILE_W >= d.out_w) return;  // block-uniform
+    const int nt = min(RT, (d.out_h - ty0 * TILE_H + TILE_H - 1) / TILE_H);
     const Sampler S = make_sampler(src, d);
-    const int y = ty * TILE_H + gy, x0 = tx * TILE_W + gx;
-    Gather4<CN> G;
-    gather4_issue<CN>(S, (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1 + (uint32_t)x0 * (uint32_t)S.b0,
-                      (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4 + (uint32_t)x0 * (uint32_t)S.b3, G);
-    uint4 px;
-    px.x = gather4_pixel<CN>(G, 0);
-    px.y = gather4_pixel<CN>(G, 1);
-    px.z = gather4_pixel<CN>(G, 2);
-    px.w = gather4_pixel<CN>(G, 3);
-    int sy = y, sx0 = x0;
-    if (PATCH) {  // restage: store pattern = ROWS map
-        stage[gy * 16 + (gx >> 2)] = px;
-        __syncthreads();
-        const int ry = (int)(threadIdx.x >> 4), rx = 4 * (int)(threadIdx.x & 15);
-        px = stage[ry * 16 + (rx >> 2)];
-        sy = ty * TILE_H + ry;
-        sx0 = tx * TILE_W + rx;
+    const int x0 = tx * TILE_W + gx;
+    Gather4<CN> G[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+        if (r < nt) {
+            const int y = (ty0 + r) * TILE_H + gy;
+            const uint32_t xx = (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1 + (uint32_t)x0 * (uint32_t)S.b0;
+            const uint32_t yy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4 + (uint32_t)x0 * (uint32_t)S.b3;
+            if (DENSE) gather4_issue_sq8<CN>(S, xx, yy, G[r]);
+            else gather4_issue<CN>(S, xx, yy, G[r]);
+        }
     }
-    if (sy >= d.out_h || sx0 >= d.out_w) return;
-    uint8_t* o = dst + d.dst_off + (int64_t)sy * d.dst_pitch + 4 * sx0;
-    if (sx0 + 4 <= d.out_w && ((reinterpret_cast<uintptr_t>(o) & 15u) == 0)) {
-        *reinterpret_cast<uint4*>(o) = px;
-    } else {
-        const uint32_t pv[4] = {px.x, px.y, px.z, px.w};
-        for (int k = 0; k < 4; ++k)
-            if (sx0 + k < d.out_w) reinterpret_cast<uint32_t*>(o)[k] = pv[k];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+        if (r >= nt) break;  // block-uniform
+        uint4 px;
+        px.x = gather4_pixel<CN>(G[r], 0);
+        px.y = gather4_pixel<CN>(G[r], 1);
+        px.z = gather4_pixel<CN>(G[r], 2);
+        px.w = gather4_pixel<CN>(G[r], 3);
+        int sy = (ty0 + r) * TILE_H + gy, sx0 = x0;
+        if (DENSE) {  // restage pixel by pixel: store pattern = ROWS map
+            if (r > 0) __syncthreads();
+            uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);
+            st32[gy * 64 + gx] = px.x;
+            st32[gy * 64 + gx + 8] = px.y;
+            st32[(gy + 8) * 64 + gx] = px.z;
+            st32[(gy + 8) * 64 + gx + 8] = px.w;
+            __syncthreads();
+            const int ry = (int)(threadIdx.x >> 4), rx = 4 * (int)(threadIdx.x & 15);
+            px = stage[ry * 16 + (rx >> 2)];
+            sy = (ty0 + r) * TILE_H + ry;
+            sx0 = tx * TILE_W + rx;
+        } else if (PATCH) {  // restage: store pattern = ROWS map
+            if (r > 0) __syncthreads();  // previous tile's stage reads done
+            stage[gy * 16 + (gx >> 2)] = px;
+            __syncthreads();
+            const int ry = (int)(threadIdx.x >> 4), rx = 4 * (int)(threadIdx.x & 15);
+            px = stage[ry * 16 + (rx >> 2)];
+            sy = (ty0 + r) * TILE_H + ry;
+            sx0 = tx * TILE_W + rx;
+        }
+        if (sy >= d.out_h || sx0 >= d.out_w) continue;
+        uint8_t* o = dst + d.dst_off + (int64_t)sy * d.dst_pitch + 4 * sx0;
+        if (sx0 + 4 <= d.out_w && ((reinterpret_cast<uintptr_t>(o) & 15u) == 0)) {
+            *reinterpret_cast<uint4*>(o) = px;
+        } else {
+            const uint32_t pv[4] = {px.x, px.y, px.z, px.w};
+            for (int k = 0; k < 4; ++k)
+                if (sx0 + k < d.out_w) reinterpret_cast<uint32_t*>(o)[k] = pv[k];
+        }
     }
 }
 
-template <bool PATCH>
+template <bool PATCH, bool DENSE = false>
 __global__ void __launch_bounds__(256)
 k_rotate_flip_nearest(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                       const ipp_gather_desc* __restrict__ descs, int tiles_x, int tiles_y) {
-    __shared__ uint4 stage[PATCH ? TILE_H * 16 : 1];
+    __shared__ uint4 stage[PATCH || DENSE ? TILE_H * 16 : 1];
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int per_img = tiles_x * tiles_y;
     const int img = b / per_img;
     const int t = b - img * per_img;
     const int ty = t / tiles_x, tx = t - ty * tiles_x;
     const ipp_gather_desc d = descs[img];
-    if (d.src_cn == 4) rotate_tile<4, PATCH>(src, dst, d, tx, ty, stage);  // block-uniform
-    else rotate_tile<3, PATCH>(src, dst, d, tx, ty, stage);
+    if (d.src_cn == 4) rotate_tiles<4, PATCH, DENSE>(src, dst, d, tx, ty, stage);  // block-uniform
+    else rotate_tiles<3, PATCH, DENSE>(src, dst, d, tx, ty, stage);
 }
 
 // Window copy with optional mirror, any bytes-per-pixel (1..4).  Each thread
@@ -215,16 +249,19 @@ extern "C" int ipp_rotate_flip_nearest(const uint8_t* src, uint8_t* dst, const i
                                        void* stream) {
     if (n_images == 0) return IPP_OK;
     if (!src || !dst || !descs || n_images < 0 || max_out_w <= 0 || max_out_h <= 0) return IPP_E_ARG;
-    const int tx = (max_out_w + TILE_W - 1) / TILE_W, ty = (max_out_h + TILE_H - 1) / TILE_H;
+    const int tx = (max_out_w + TILE_W - 1) / TILE_W, ty = (max_out_h + TILE_H * RT - 1) / (TILE_H * RT);
     const int64_t blocks = (int64_t)tx * ty * n_images;
     if (!grid_ok(blocks)) return IPP_E_ARG;
     static const int map = [] {
-        const char* e = getenv("IPP_GATHER_MAP");  // 0 rows, 1 patch + LDS restage
-        return e ? atoi(e) : 1;
+        const char* e = getenv("IPP_GATHER_MAP");  // 0 rows, 1 patch + LDS restage, 2 dense 8×8 + restage
+        return e ? atoi(e) : 2;
     }();
     if (map == 0)
         hipLaunchKernelGGL(k_rotate_flip_nearest<false>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
                            src, dst, descs, tx, ty);
+    else if (map == 2)
+        hipLaunchKernelGGL((k_rotate_flip_nearest<false, true>), dim3((uint32_t)blocks), dim3(256), 0,
+                           (hipStream_t)stream, src, dst, descs, tx, ty);
     else
         hipLaunchKernelGGL(k_rotate_flip_nearest<true>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
                            src, dst, descs, tx, ty);

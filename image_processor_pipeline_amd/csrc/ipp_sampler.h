@@ -70,3 +70,31 @@ __device__ __forceinline__ uint32_t gather4_pixel(const Gather4<CN>& G, int k) {
     const uint32_t p = CN == 3 ? ((G.raw[k] >> G.sh[k]) | 0xFF000000u) : G.raw[k];
     return ((G.valid >> k) & 1u) ? p : 0u;
 }
+
+// Four M pixels at the corners of an 8×8 square: (0,0), (0,8), (8,0), (8,8)
+// (x, y offsets).  With lanes laid out as 8 rows × 8 columns, each load
+// instruction then reads one dense 8×8 block: a compact source footprint
+// (fewer cache lines per wave instruction than 16 rows × 4 spread columns).
+template <int CN>
+__device__ __forceinline__ void gather4_issue_sq8(const Sampler& S, uint32_t xx, uint32_t yy, Gather4<CN>& G) {
+    G.valid = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t xk = xx + (k & 1) * 8u * (uint32_t)S.b0 + (k >> 1) * 8u * (uint32_t)S.b1;
+        const uint32_t yk = yy + (k & 1) * 8u * (uint32_t)S.b3 + (k >> 1) * 8u * (uint32_t)S.b4;
+        const int xin = (int32_t)xk >> 16, yin = (int32_t)yk >> 16;
+        const bool ok = ((uint32_t)xin < (uint32_t)S.in_w) & ((uint32_t)yin < (uint32_t)S.in_h);
+        const uint32_t off_any = (uint32_t)__umul24(yin, S.pitch) + (uint32_t)__umul24(xin, CN);
+        uint32_t off = ok ? off_any : 0u;
+        if (CN == 3) {
+            const uint32_t offc = min(off, S.lim);
+            G.sh[k] = (off - offc) << 3;
+            off = offc;
+        }
+#ifdef IPP_DBG_ALIGNED_GATHER
+        off &= ~3u;  // diagnostics (wrong output): aligned dword gathers
+#endif
+        G.raw[k] = *reinterpret_cast<const ipp_u32_unaligned*>(S.base + off);
+        G.valid |= (ok ? 1u : 0u) << k;
+    }
+}
