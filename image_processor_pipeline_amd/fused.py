@@ -33,6 +33,7 @@ from .device import SYM_FLIP, _stream, _to_dev
 ALL_SYMS = ("o", "h", "v", "hv")
 # H-pass tap format: "mfma" (v_mfma_i32_16x16x64_i8 tiles) or "dot4" (VALU)
 TAPS = os.environ.get("IPP_TAPS", "mfma")
+H_RING_COLUMNS = 512   # ipp_pipe.hip RING
 
 
 @dataclass
@@ -177,6 +178,16 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
                    for j in range(m)], np.int64)
     ngs = np.array([lib.ipp_plan_dot4_stride(int(k)) for k in ks], np.int64)
     mfma = TAPS == "mfma"
+    # The H pass keeps each output tile's input window in a 512-column LDS ring
+    # (ipp_pipe.hip RING): 64·nK columns (mfma) or 4·ngs (dot4) must fit.
+    for j in range(0, m, 2):
+        if ident[j]:
+            continue
+        cols = (64 * lib.ipp_plan_mfma_nk_bound(int(a_in[j]), int(a_out[j]), int(ks[j])) if mfma
+                else 4 * int(ngs[j]))
+        if cols > H_RING_COLUMNS:
+            raise ValueError(f"item {j // 2}: LANCZOS downscale {a_in[j]} -> {a_out[j]} needs a {cols}-column "
+                             f"window, more than the fused H pass holds ({H_RING_COLUMNS}); use the plugin path")
     # H axes (even j): mfma tiles or transposed dot4; V axes: row-major dot4
     # (V axes in mfma form: tiles aligned with 16-row background bands, phase = y mod 16)
     transp = np.array([(2 if mfma else 1) if j % 2 == 0 else ((2 + params[j // 2].y % 16) if mfma else 0)

@@ -266,6 +266,18 @@ def test_pipe_split_equals_unsplit(D):
             assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (bw, i)
 
 
+def test_pipe_crop_reaching_source_end(D):
+    """Zero bottom/right margins: the crop window ends at the source's last
+    byte, so the last pixel's 4-byte gather would cross the image (and, for
+    the last item, the allocation) end — the H pass takes its clamped path."""
+    from image_processor_pipeline_amd import fused
+    for margins in [(3, 0, 5, 0), (0, 0, 0, 0)]:
+        cfg = fused.PipeConfig(margins=margins, scale_min=0.3, scale_max=0.7)
+        src, bgs, plan, got = _run_pipe(5, 70, 90, 2, 80, 96, cfg, seed=21)
+        for i in range(len(got)):
+            assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (margins, i)
+
+
 def test_pipe_fullsize_items_vs_oracle(D):
     """BASELINE config 3 geometry (1024² sources, 64-px margins, 1024² bgs)."""
     from image_processor_pipeline_amd import fused

@@ -157,3 +157,13 @@ def test_mfma_tile_format_is_exact(io, shift, phase):
             ref = (1 << 21) + int((pix[xmin:xmin + cnt].astype(np.int64) * std[2 * o + oo * k:2 * o + oo * k + cnt]).sum())
             got = int(bias[16 * t + col]) + int(acc[0, col]) + (int(acc[1, col]) << 8) + (int(acc[2, col]) << 16)
             assert got == ref, (t, col)
+
+
+def test_pipe_plan_rejects_windows_wider_than_the_ring():
+    """A downscale whose tap window exceeds the H pass's 512-column LDS ring is
+    refused at planning time (no silent window overrun on the device)."""
+    from image_processor_pipeline_amd import fused
+    with pytest.raises(ValueError, match="window"):
+        fused.plan_pipe((1024, 1024), 2, (1024, 1024), 1, fused.PipeConfig(scale_min=0.01, scale_max=0.012), seed=0)
+    plan = fused.plan_pipe((1024, 1024), 2, (1024, 1024), 1, fused.PipeConfig(), seed=0)
+    assert plan.max_ov_h >= 1 and plan.algo_bytes_hpass_bgcopy > plan.algo_bytes_hpass
