@@ -40,6 +40,8 @@
 // chain); everything else is per component.
 #include <algorithm>
 
+#include <type_traits>
+
 #include "ipp_hsv.h"
 
 namespace {
@@ -185,7 +187,8 @@ k_ccl_tile(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ d
     __shared__ uint32_t area[TPX];
     __shared__ unsigned long long cols[TPX];  // per root: mask of its columns
     __shared__ unsigned long long rowbits[TH];
-    __shared__ int32_t sdiv[SRC == SRC_HSV ? 256 : 1], hdiv[SRC == SRC_HSV ? 256 : 1];
+    struct NoTables {};
+    __shared__ typename std::conditional<SRC == SRC_HSV, HsvTables<NR>, NoTables>::type T;
     __shared__ int nroots, base;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int im = b / tiles_per_img;
@@ -199,11 +202,10 @@ k_ccl_tile(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ d
     const int x = tx * TW + lane;
     const unsigned long long below = (1ull << lane) - 1ull;
 
-    Ranges<SRC == SRC_HSV ? NR : 1> R;
-    if (SRC == SRC_HSV) {
-        sdiv[threadIdx.x] = kSdiv[threadIdx.x];
-        hdiv[threadIdx.x] = kHdiv180[threadIdx.x];
-        ranges_init<SRC == SRC_HSV ? NR : 1, ZONES>(R, hp, d.w, d.h);
+    Ranges<SRC == SRC_HSV ? NR : 1> R;  // zones only (the test itself is table-driven)
+    if constexpr (SRC == SRC_HSV) {
+        hsv_tables_init<NR>(T, hp);
+        if (ZONES) ranges_init<NR, ZONES>(R, hp, d.w, d.h);
         __syncthreads();
     }
     if (threadIdx.x == 0) nroots = 0;
@@ -223,7 +225,18 @@ k_ccl_tile(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ d
             } else {
                 const bool wide_ok = (y < d.h - 1) || (x < d.w - 1);
                 const uint32_t px = load_rgb_opaque(row + 3 * x, wide_ok);
-                fg = hsv_keep<SRC == SRC_HSV ? NR : 1, ZONES, true>(R, sdiv, hdiv, px, x, y) != 0u;
+                if constexpr (SRC == SRC_HSV) {
+                    uint32_t ex = hsv_tab_excl<NR, true>(T, px);
+                    if (ZONES) {
+                        uint32_t zb = 0;
+#pragma unroll
+                        for (int q = 0; q < NR; ++q)
+                            zb |= (uint32_t)(((uint32_t)(y - R.r0[q]) < (uint32_t)R.rh[q]) &
+                                             ((uint32_t)(x - R.c0[q]) < (uint32_t)R.cw[q])) << q;
+                        ex &= zb;
+                    }
+                    fg = ex == 0u;
+                }
             }
         }
         const unsigned long long bits = __ballot(fg);

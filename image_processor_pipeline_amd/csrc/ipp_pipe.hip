@@ -319,34 +319,16 @@ k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
 //     OpenCV's h < 0 → h + 180 wrap into the table.
 // ---------------------------------------------------------------------------
 template <int NR>
-struct MaskType { typedef uint8_t T; };
-template <>
-struct MaskType<IPP_MAX_HSV_RANGES> { typedef uint16_t T; };
-
-constexpr int HMN = 192;  // hm entries: h + 32 ∈ [2, 182]
-
-template <int NR>
 struct __attribute__((aligned(16))) Hpass2Lds {
     typedef typename MaskType<NR>::T MT;
     uint8_t win[4][HR][WSTRIDE];   // planar window ring, bytes p ^ 0x80
-    uint32_t sv[256];              // sdiv[v]
-    int32_t hd[256];               // hdiv[diff]
-    MT vm[256], sm[256], hm[HMN];  // per-channel range masks
+    HsvTables<NR> T;               // table-driven HSV test (ipp_hsv.h)
 };
 
 // M pixel → window byte quad (p | α 255) ^ 0x80 when kept, 0x80808080 (transparent black) when excluded.
 template <int NR, bool ZONES>
 __device__ __forceinline__ uint32_t hsv2_px(const Hpass2Lds<NR>& L, uint32_t raw, uint32_t zbits) {
-    const uint32_t r = raw & 0xFFu, g = (raw >> 8) & 0xFFu, b = (raw >> 16) & 0xFFu;
-    const uint32_t v = max(max(r, g), b);
-    const uint32_t d = v - min(min(r, g), b);
-    const uint32_t s = mad_u24(d, L.sv[v], 2048u) >> 12;
-    // OpenCV's hue numerator: v==r ? g-b : v==g ? b-r+2d : r-g+4d
-    const int nr = (int)g - (int)b, ng = (int)b - (int)r + 2 * (int)d, nb = (int)r - (int)g + 4 * (int)d;
-    int n = (v == g) ? ng : nb;
-    n = (v == r) ? nr : n;
-    const uint32_t hi = (uint32_t)mad_i24(n, L.hd[d], 2048 + (32 << 12)) >> 12;
-    uint32_t ex = (uint32_t)L.vm[v] & (uint32_t)L.sm[s] & (uint32_t)L.hm[hi];
+    uint32_t ex = hsv_tab_excl<NR, false>(L.T, raw);
     if (ZONES) ex &= zbits;
     const uint32_t t = (raw | 0xFF000000u) ^ 0x80808080u;
     return ex ? 0x80808080u : t;
@@ -658,7 +640,6 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
               const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp, const uint8_t* __restrict__ bg,
               uint8_t* __restrict__ dst, int cpi) {
     __shared__ Hpass2Lds<NR> L;
-    typedef typename MaskType<NR>::T MT;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     // COPY: each item owns tiles_y H-pass blocks followed by cpi background-copy
     // blocks, so copies run beside the VALU-bound H pass on every XCD.
@@ -675,24 +656,7 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
     if (row0 >= h.lines) return;  // block-uniform
 
     // Tables (one entry per thread, hm: 192 entries).
-    {
-        const int i = threadIdx.x;
-        uint32_t vmk = 0, smk = 0, hmk = 0;
-        int hh = i - 32;
-        hh = hh < 0 ? hh + 180 : hh;
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            const ipp_hsv_range& q = hp.r[k];
-            vmk |= (uint32_t)(i >= q.lo[2] && i <= q.hi[2]) << k;
-            smk |= (uint32_t)(i >= q.lo[1] && i <= q.hi[1]) << k;
-            hmk |= (uint32_t)(hh >= q.lo[0] && hh <= q.hi[0]) << k;
-        }
-        L.sv[i] = (uint32_t)kSdiv[i];
-        L.hd[i] = kHdiv180[i];
-        L.vm[i] = (MT)vmk;
-        L.sm[i] = (MT)smk;
-        if (i < HMN) L.hm[i] = (MT)hmk;
-    }
+    hsv_tables_init<NR>(L.T, hp);
 
     // Zones: per-lane row bits now, column bits per pixel.
     int32_t zc0[ZONES ? NR : 1], zcw[ZONES ? NR : 1];
