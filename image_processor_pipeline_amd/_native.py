@@ -106,6 +106,8 @@ SIGNATURES = {
     "ipp_plan_mfma_from_taps": (_I, [_I, _I, _I, _P, _I, _I, _P]),
     "ipp_plan_mfma_nk_bound": (_I, [_I, _I, _I]),
     "ipp_plan_pipe_axes": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I]),
+    "ipp_stream_copy": (_I, [_P, _P, _L, _P]),
+    "ipp_pipe_status": (_I, [_P, _P]),
     "ipp_version": (ctypes.c_char_p, []),
 }
 

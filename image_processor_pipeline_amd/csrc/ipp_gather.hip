@@ -252,10 +252,14 @@ extern "C" int ipp_rotate_flip_nearest(const uint8_t* src, uint8_t* dst, const i
     const int tx = (max_out_w + TILE_W - 1) / TILE_W, ty = (max_out_h + TILE_H * RT - 1) / (TILE_H * RT);
     const int64_t blocks = (int64_t)tx * ty * n_images;
     if (!grid_ok(blocks)) return IPP_E_ARG;
-    static const int map = [] {
-        const char* e = getenv("IPP_GATHER_MAP");  // 0 rows, 1 patch + LDS restage, 2 dense 8×8 + restage
+#ifdef IPP_DIAG
+    static const int map = [] {  // experiment: 0 rows, 1 patch + LDS restage, 2 dense 8×8 + restage
+        const char* e = getenv("IPP_GATHER_MAP");
         return e ? atoi(e) : 2;
     }();
+#else
+    constexpr int map = 2;
+#endif
     if (map == 0)
         hipLaunchKernelGGL(k_rotate_flip_nearest<false>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
                            src, dst, descs, tx, ty);

@@ -9,18 +9,19 @@
 // filtres_liste.py:84-134 → overlays.py:129,138-139.  The RGBA cut-out "M" is
 // never materialised: the LANCZOS horizontal pass computes each M pixel on the
 // fly from the source (gather → HSV α → premultiply) into a channel-planar
-// LDS window and runs the taps over it with v_dot4c_i32_i8; the vertical pass
-// is fused with unpremultiply, the alpha blend and the background copy.
+// LDS window and runs the taps over it on the matrix cores
+// (v_mfma_i32_16x16x64_i8); the vertical pass (MFMA too) is fused with
+// unpremultiply, the alpha blend and the background copy.
 //
 // Exact integer arithmetic (Pillow Resample.c): each 22-bit tap k is split into
 // three balanced signed bytes (k = k0 + 256 k1 + 65536 k2) and every pixel p is
 // stored as p ^ 0x80 (= p - 128 as int8), so
-//   2^21 + Σ p·k = bias + Σ_b 2^(8b) Σ_j sdot4(p4_j, kb_j),  bias = 2^21 + 128 Σk
-// holds bit-for-bit (ipp_host.cpp ipp_plan_dot4_from_taps builds the planes).
+//   2^21 + Σ p·k = bias + Σ_b 2^(8b) Σ_j p_j·kb_j,  bias = 2^21 + 128 Σk
+// holds bit-for-bit (ipp_host.cpp builds the tap tiles and the bias).
 //
 // T (H-pass output) layout per item: [row group g][column x'][4 channels][4
-// rows] bytes (16 B per (g, x')), values XOR 0x80, so the V pass reads one
-// dwordx4 per 4 taps per pixel.  T rows are M rows [line0, line0 + lines).
+// rows] bytes (16 B per (g, x')), values XOR 0x80.  T rows are M rows
+// [line0, line0 + lines).
 #include <algorithm>
 
 #include "ipp_hsv.h"
@@ -28,34 +29,27 @@
 
 namespace {
 
-constexpr int HX = 64;            // H-pass outputs per chunk (one per lane)
 constexpr int HR = 16;            // H-pass rows per block (4 per thread)
 constexpr int RING = 512;         // window ring: M columns x live at x & (RING - 1)
 constexpr int WSTRIDE = 528;      // LDS bytes per plane row (≡ 4 dwords mod 32 banks)
-constexpr int VR = 4;             // composite rows per vblend block
-// ipp_pipe_hpass_bgcopy: background-copy blocks per item (IPP_COPY_BLOCKS overrides)
+// ipp_pipe_hpass_bgcopy: background-copy blocks per item.  Diagnostic builds
+// (-DIPP_DIAG) may override it and select the experiment kernels below through
+// environment variables; the product build reads no environment at all.
+#ifdef IPP_DIAG
+inline int diag_env(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
 inline int copy_blocks_per_item() {
     static const int v = [] {
-        const char* e = getenv("IPP_COPY_BLOCKS");
-        const int k = e ? atoi(e) : 4;
+        const int k = diag_env("IPP_COPY_BLOCKS", 4);
         return k < 1 ? 1 : (k > 64 ? 64 : k);
     }();
     return v;
 }
-
-__device__ __forceinline__ int32_t sdot4(uint32_t a, uint32_t b, int32_t c) {
-#ifdef IPP_DBG_NO_DOT4
-    int32_t s = c;
-    for (int i = 0; i < 4; ++i) s += (int32_t)(int8_t)(a >> (8 * i)) * (int32_t)(int8_t)(b >> (8 * i));
-    return s;
-#elif defined(IPP_DBG_VOP3P)
-    int32_t d;
-    asm("v_dot4_i32_i8 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
 #else
-    return __builtin_amdgcn_sdot4((int32_t)a, (int32_t)b, c, false);
+constexpr int copy_blocks_per_item() { return 4; }
 #endif
-}
 
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
     return __builtin_amdgcn_perm(hi, lo, sel);
@@ -71,237 +65,7 @@ __device__ __forceinline__ void transpose4(uint32_t p0, uint32_t p1, uint32_t p2
     ch[3] = perm(hi23, hi01, 0x07060302u);
 }
 
-#ifdef IPP_DBG_DUMP
-__device__ uint8_t g_dbg_win[4 * 16 * 400];
-__device__ int32_t g_dbg_meta[8];
-#endif
-
-struct __attribute__((aligned(16))) HpassLds {
-    uint8_t win[4][HR][WSTRIDE];      // planar window ring, bytes p ^ 0x80
-    int32_t sdiv[256], hdiv[256];     // OpenCV RGB2HSV_b division tables
-};
-
-// One block = one 16-row band of one item, sweeping all its outputs in chunks
-// of ≤ 64.  The M window is a ring of RING columns: each chunk only computes
-// the columns its predecessor did not (consecutive chunks' windows overlap by
-// the filter support), so every M pixel of the band is gathered and
-// HSV-tested exactly once.
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
-
-template <int NR, bool ZONES, int CN, int FMT, int DBG = 0>
-__global__ void __launch_bounds__(256)
-k_pipe_hpass(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
-             const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp) {
-    __shared__ HpassLds L;
-    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / tiles_y;
-    const int ty = b - im * tiles_y;
-    const ipp_gather_desc g = descs[im].g;
-    const ipp_resample_desc h = descs[im].h;
-    const int row0 = ty * HR;
-    if (row0 >= h.lines) return;  // block-uniform
-
-    for (int i = threadIdx.x; i < 256; i += 256) {
-        L.sdiv[i] = kSdiv[i];
-        L.hdiv[i] = kHdiv180[i];
-    }
-    Ranges<NR> R;
-    ranges_init<NR, ZONES>(R, hp, g.out_w, g.out_h);
-    const Sampler S = make_sampler(src, g);
-    const int ngs = h.ksize;  // tap-group stride of this item (dot4 format)
-    const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
-    // dot4: H tap planes are stored transposed, [group j][output x'] (16 B each),
-    // so a wave's 64 lanes read one contiguous KiB per group.
-    const uint4* planes = reinterpret_cast<const uint4*>(coefs + h.coef_off + 4 * (int64_t)h.out_len);
-    // mfma: tile headers (K0, nK, boff), per-output bias, B blocks (ipp_host.cpp)
-    const int ntiles = (h.out_len + 15) >> 4;
-    const int32_t* tbias = coefs + h.coef_off + 4 * (int64_t)ntiles;
-    const uint4* tblk = reinterpret_cast<const uint4*>(coefs + h.coef_off + 20 * (int64_t)ntiles);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform → SGPR
-    const int nrows = min(HR, h.lines - row0);
-
-    // Phase-1 lane geometry: a wave covers 16 rows × 16 px per step.
-    const int r = lane >> 2;
-    const int y = h.line0 + row0 + r;
-    const uint32_t rowx = (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1;
-    const uint32_t rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
-
-    int filled = hdr[0].x;  // ring holds M columns [.., filled)
-    // Chunks: dot4 — up to HX outputs, one per lane; mfma — up to 4 tiles of 16
-    // outputs, one per wave.  A chunk's window must fit the ring.
-    const int nunits = FMT == 0 ? h.out_len : ntiles;
-    for (int s0 = 0; s0 < nunits;) {
-        int s1, W0, W1;
-        if (FMT == 0) {
-            s1 = min(s0 + HX, h.out_len);
-            while (s1 - s0 > 1 && hdr[s1 - 1].x + 4 * ngs - hdr[s0].x > RING) s1 = s0 + (s1 - s0 + 1) / 2;
-            W0 = hdr[s0].x;
-            W1 = hdr[s1 - 1].x + 4 * ngs;  // window end (multiple of 4)
-        } else {
-            W0 = hdr[s0].x;
-            s1 = min(s0 + 4, ntiles);
-            for (;;) {
-                W1 = W0;
-                for (int t = s0; t < s1; ++t) W1 = max(W1, hdr[t].x + 64 * hdr[t].y);
-                if (s1 - s0 == 1 || W1 - W0 <= RING) break;
-                --s1;
-            }
-        }
-        const int c0 = max(filled, W0);  // first column not in the ring
-        const int ng4 = max(0, (W1 - c0) >> 2);
-        filled = max(filled, W1);
-
-        if (s0 == 0) __syncthreads();  // HSV tables visible
-
-        // Phase 1: new M columns → planar LDS ring; next step's gathers are in
-        // flight while this step's HSV runs.
-        Gather4<CN> cur, nxt;
-        int cg0 = wave * 4;
-        if (cg0 < ng4) {
-            const int x = c0 + 4 * (cg0 + (lane & 3));
-            if (DBG & 4) { nxt.valid = 15u; for (int k = 0; k < 4; ++k) { nxt.raw[k] = x * 2654435761u + k; nxt.sh[k] = 0; } }
-            else gather4_issue<CN>(S, rowx + (uint32_t)x * (uint32_t)S.b0, rowy + (uint32_t)x * (uint32_t)S.b3, nxt);
-        }
-        for (; cg0 < ng4; cg0 += 16) {
-            cur = nxt;
-            const int cg = cg0 + (lane & 3);
-            const int x = c0 + 4 * cg;
-            if (cg0 + 16 < ng4) {
-                const int xn = x + 64;
-                if (DBG & 4) { nxt.valid = 15u; for (int k = 0; k < 4; ++k) { nxt.raw[k] = xn * 2654435761u + k + y; nxt.sh[k] = 0; } }
-                else gather4_issue<CN>(S, rowx + (uint32_t)xn * (uint32_t)S.b0, rowy + (uint32_t)xn * (uint32_t)S.b3, nxt);
-            }
-            const bool active = (cg < ng4) && (r < nrows);
-            uint32_t px[4];
-            if (__ballot(cur.valid != 0u && active) != 0ull) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t p = gather4_pixel<CN>(cur, k);
-                    px[k] = (DBG & 1) ? (p | 0xFF000000u) : keep_pixel(p, hsv_keep<NR, ZONES>(R, L.sdiv, L.hdiv, p, x + k, y));
-                }
-            } else {
-                // all-fill wave: HSV of black is constant, only zones vary
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    px[k] = keep_pixel(0u, hsv_keep<NR, ZONES>(R, L.sdiv, L.hdiv, 0u, x + k, y));
-            }
-            if (active) {
-                uint32_t ch[4];
-                transpose4(px[0], px[1], px[2], px[3], ch);
-                const int pos = x & (RING - 1);
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    *reinterpret_cast<uint32_t*>(&L.win[c][r][pos]) = ch[c] ^ 0x80808080u;
-            }
-        }
-        __syncthreads();
-
-        if (FMT == 0) {
-            // Phase 2: output x' = s0 + lane, rows 4*wave .. 4*wave+3.
-            const int xo = s0 + lane;
-            if (xo < s1) {
-                const int4 hd = hdr[xo];
-                int32_t acc[4][4][3];
-    #pragma unroll
-                for (int rr = 0; rr < 4; ++rr)
-    #pragma unroll
-                    for (int c = 0; c < 4; ++c) acc[rr][c][0] = acc[rr][c][1] = acc[rr][c][2] = 0;
-                auto step = [&](int pos, const uint4 tp) {
-    #pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        const int row = 4 * wave + rr;
-    #pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            const uint32_t w = *reinterpret_cast<const uint32_t*>(&L.win[c][row][pos]);
-                            acc[rr][c][0] = sdot4(w, tp.x, acc[rr][c][0]);
-                            acc[rr][c][1] = sdot4(w, tp.y, acc[rr][c][1]);
-                            acc[rr][c][2] = sdot4(w, tp.z, acc[rr][c][2]);
-                        }
-                    }
-                };
-                // One tap group per iteration: unrolling j lets the compiler merge
-                // the 4-byte-aligned window reads of j and j+1 into ds_read2_b64,
-                // which gfx950 replays at ~64 cycles when not 8-byte aligned.
-                const uint4* tpg = planes + xo;
-                uint4 tp = tpg[0];
-    #pragma unroll 1
-                for (int j = 0; j < ngs; ++j) {
-                    const uint4 cur = tp;
-                    if (j + 1 < ngs) tp = tpg[(int64_t)(j + 1) * h.out_len];  // prefetch next group
-                    step((hd.x + 4 * j) & (RING - 1), cur);
-                }
-                uint32_t outc[4] = {0u, 0u, 0u, 0u};
-    #pragma unroll
-                for (int rr = 0; rr < 4; ++rr)
-    #pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        const int32_t ss = hd.z + acc[rr][c][0] + (acc[rr][c][1] << 8) + (acc[rr][c][2] << 16);
-                        outc[c] |= clip8(ss) << (8 * rr);
-                    }
-                const int grp = (row0 >> 2) + wave;
-                uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
-                *dst = make_uint4(outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
-                                  outc[3] ^ 0x80808080u);
-            }
-        } else {
-            // Phase 2 (mfma): wave w takes tile s0 + w; A = 16 window rows × 64
-            // columns of one channel (lane l: row l&15, bytes 16(l>>4)..+15),
-            // B = 64 columns × 16 outputs of one tap byte plane.  D lane l =
-            // output l&15, rows 4(l>>4)..+3 = exactly one 16-B T group.
-            const int t = s0 + wave;
-            if (!(DBG & 2) && t < s1) {
-                const int4 th = hdr[t];
-                i32x4 acc[4][3];
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) acc[c][p] = i32x4{0, 0, 0, 0};
-                const uint4* bt = tblk + th.z + lane;
-                const int arow = lane & 15, akoff = 16 * (lane >> 4);
-                uint4 bn[3];
-#pragma unroll
-                for (int p = 0; p < 3; ++p) bn[p] = bt[p * 64];
-#pragma unroll 1
-                for (int ks = 0; ks < th.y; ++ks) {
-                    i32x4 bq[3];
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) bq[p] = __builtin_bit_cast(i32x4, bn[p]);
-                    if (ks + 1 < th.y) {
-#pragma unroll
-                        for (int p = 0; p < 3; ++p) bn[p] = bt[((ks + 1) * 3 + p) * 64];
-                    }
-                    const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        const i32x4 a = *reinterpret_cast<const i32x4*>(&L.win[c][arow][pos]);
-#pragma unroll
-                        for (int p = 0; p < 3; ++p)
-                            acc[c][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[p], acc[c][p], 0, 0, 0);
-                    }
-                }
-                const int xo = 16 * t + (lane & 15);
-                if (xo < h.out_len) {
-                    const int32_t bias = tbias[xo];
-                    uint32_t outc[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-                    for (int c = 0; c < 4; ++c)
-#pragma unroll
-                        for (int rr = 0; rr < 4; ++rr) {
-                            const int32_t ss = bias + acc[c][0][rr] + (acc[c][1][rr] << 8) + (acc[c][2][rr] << 16);
-                            outc[c] |= clip8(ss) << (8 * rr);
-                        }
-                    const int grp = (row0 >> 2) + (lane >> 4);
-                    uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
-                    *dst = make_uint4(outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
-                                      outc[3] ^ 0x80808080u);
-                }
-            }
-        }
-        __syncthreads();
-        s0 = s1;
-    }
-}
 
 // ---------------------------------------------------------------------------
 // H pass v2 (MFMA taps): table-driven HSV test and buffer-load gathers.
@@ -377,6 +141,11 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
 }
 
 // One chunk of ≤ 4 output tiles whose input window fits the ring.
+// Sticky status of the pipe kernels (ipp_pipe_status): bit 0 = an H-pass
+// output tile's input window was wider than the LDS ring (the plan violated
+// the ring limit of ipp.h; that tile's T columns are wrong).
+__device__ int32_t g_pipe_status;
+
 struct Hp2Chunk {
     int s0, s1;   // tiles [s0, s1)
     int c0;       // first M column not yet in the ring
@@ -396,6 +165,7 @@ __device__ __forceinline__ Hp2Chunk hp2_chunk(const int4* hdr, int s0, int ntile
         --s1;
     }
     c.s1 = s1;
+    if (W1 - W0 > RING && threadIdx.x == 0) atomicOr(&g_pipe_status, 1);  // single tile beyond the ring
     c.c0 = max(filled, W0);
     c.ng4 = max(0, (W1 - c.c0) >> 2);
     c.nsteps = c.ng4 > wave * 4 ? (c.ng4 - wave * 4 + 15) >> 4 : 0;
@@ -733,83 +503,6 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
 
 }
 
-// V pass over T (dot4) → unpremultiply → blend onto the background, fused with
-// the background copy.  Block = VR composite rows.
-template <int STORE>
-__global__ void __launch_bounds__(256)
-k_pipe_vblend(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
-              const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int tiles_y, int bg_w_max) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t orow[];  // [VR][bg_w_max]
-    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / tiles_y;
-    const int ty = b - im * tiles_y;
-    const ipp_resample_desc v = descs[im].v;
-    const ipp_paste_desc p = descs[im].p;
-    const int y0 = ty * VR;
-    if (y0 >= p.bg_h) return;
-    const int nrows = min(VR, p.bg_h - y0);
-
-    // Phase 1: overlay rows of this band.
-    const int ngs = v.ksize;
-    const int4* hdr = reinterpret_cast<const int4*>(coefs + v.coef_off);
-    const uint4* planes = reinterpret_cast<const uint4*>(coefs + v.coef_off + 4 * (int64_t)v.out_len);
-    bool any = false;
-    for (int r = 0; r < nrows; ++r) {
-        const int oy = y0 + r - p.y;
-        if ((unsigned)oy >= (unsigned)p.ov_h) continue;
-        any = true;
-        const int4 hd = hdr[oy];
-        const uint4* tp = planes + (int64_t)oy * ngs;
-        const uint4* col0 = reinterpret_cast<const uint4*>(tmp + v.src_off + (int64_t)(hd.x >> 2) * v.src_pitch);
-        const int gstride = v.src_pitch >> 4;
-        for (int x = threadIdx.x; x < p.ov_w; x += 256) {
-            int32_t acc[4][3];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc[c][0] = acc[c][1] = acc[c][2] = 0;
-            const uint4* q = col0 + x;
-            for (int j = 0; j < ngs; ++j) {
-                const uint4 w = q[(int64_t)j * gstride];
-                const uint4 k = tp[j];
-                const uint32_t wc[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    acc[c][0] = sdot4(wc[c], k.x, acc[c][0]);
-                    acc[c][1] = sdot4(wc[c], k.y, acc[c][1]);
-                    acc[c][2] = sdot4(wc[c], k.z, acc[c][2]);
-                }
-            }
-            uint32_t o = 0;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) o |= clip8(hd.z + acc[c][0] + (acc[c][1] << 8) + (acc[c][2] << 16)) << (8 * c);
-            orow[r * bg_w_max + x] = unpremultiply(o);
-        }
-    }
-    if (any) __syncthreads();
-
-    // Phase 2: composite rows = background bytes, blended inside the footprint.
-    const int row_bytes = 3 * p.bg_w;
-    const int chunks = (row_bytes + 15) >> 4;
-    for (int r = 0; r < nrows; ++r) {
-        const int y = y0 + r;
-        const uint8_t* brow = bg + p.bg_off + (int64_t)y * p.bg_pitch;
-        uint8_t* drow = dst + p.dst_off + (int64_t)y * p.dst_pitch;
-        const int oy = y - p.y;
-        const bool in_rows = (unsigned)oy < (unsigned)p.ov_h;
-        const uint32_t* orw = orow + r * bg_w_max;
-        for (int ci = threadIdx.x; ci < chunks; ci += 256) {
-            const int c0 = ci << 4;
-            const int nbytes = min(16, row_bytes - c0);
-            const bool vec = nbytes == 16 &&
-                             ((reinterpret_cast<uintptr_t>(brow + c0) | reinterpret_cast<uintptr_t>(drow + c0)) & 15u) == 0;
-            uint32_t w[4];
-            load16(brow + c0, nbytes, vec, w);
-            if (in_rows && c0 + nbytes > 3 * p.x && c0 < 3 * (p.x + p.ov_w))
-                blend16(w, c0, nbytes, p.x, p.ov_w, [&](int ox) { return orw[ox]; });
-            store16<STORE>(drow + c0, nbytes, vec, w);
-        }
-    }
-}
-
 // V pass on MFMA (tap tiles aligned with 16-row background bands: the plan's
 // phase = p.y mod 16) → unpremultiply → blend onto the background, fused with
 // the background copy.  Block = 16 composite rows of one item.  A = taps of
@@ -939,77 +632,47 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
 
 template <int NR, bool ZONES, int CN>
 void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
-                  const ipp_pipe_desc* descs, int fmt, int ty, const ipp_hsv_params& hp, const uint8_t* bg,
-                  uint8_t* dst) {
-    static const int dbg = [] {
-        const char* e = getenv("IPP_DBG_HPASS");  // diagnostics (wrong output): 1 no HSV, 2 no H taps, 3 neither
-        return e ? atoi(e) : 0;
-    }();
-    static const int impl = [] {
-        const char* e = getenv("IPP_HPASS");  // 1: previous (packed-compare HSV) kernel
-        return e ? atoi(e) : 2;
-    }();
+                  const ipp_pipe_desc* descs, int ty, const ipp_hsv_params& hp, const uint8_t* bg, uint8_t* dst) {
     if (bg && dst) {  // H pass + the background rows outside the overlay bands
-        if (fmt != IPP_TAPS_MFMA) return;  // rejected by the entry point
-        const dim3 g2((uint32_t)(grid.x / ty * (ty + copy_blocks_per_item())));
-        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 0, true>), g2, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg,
-                           dst, copy_blocks_per_item());
-    } else if (fmt == IPP_TAPS_MFMA && dbg == 0 && impl == 2)
-        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0);
-    else if (fmt == IPP_TAPS_MFMA && impl == 2 && dbg >= 10 && (NR == 4 && !ZONES && CN == 3)) {
-        // diagnostics (wrong output): 10+d, d bit0 coalesced gathers, bit1 no HSV, bit2 no phase 2;
-        // 18: no fill-step skipping (correct output)
+        const int cpi = copy_blocks_per_item();
+        const dim3 g2((uint32_t)(grid.x / ty * (ty + cpi)));
+        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 0, true>), g2, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp,
+                           bg, dst, cpi);
+        return;
+    }
+#ifdef IPP_DIAG
+    // Experiment kernels (WRONG output): IPP_DBG_HPASS = 10 + d, d bit0
+    // coalesced gathers, bit1 no HSV, bit2 no phase 2, bit3 no fill-step
+    // skipping, bit4 cache-resident scatter.
+    static const int dbg = diag_env("IPP_DBG_HPASS", 0);
+    if (dbg >= 10 && NR == 4 && !ZONES && CN == 3) {
         switch (dbg - 10) {
-            case 1: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
-            case 2: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 2>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
-            case 3: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 3>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
-            case 4: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 4>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
-            case 5: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 5>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
-            case 6: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 6>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
-            case 7: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 7>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
-            case 16: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 16>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
-            case 20: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 20>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
-            default: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 8>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); break;
+#define IPP_DIAG_CASE(D) \
+    case D: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, D>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); return;
+            IPP_DIAG_CASE(1) IPP_DIAG_CASE(2) IPP_DIAG_CASE(3) IPP_DIAG_CASE(4) IPP_DIAG_CASE(5) IPP_DIAG_CASE(6)
+            IPP_DIAG_CASE(7) IPP_DIAG_CASE(8) IPP_DIAG_CASE(16) IPP_DIAG_CASE(20)
+#undef IPP_DIAG_CASE
+            default: break;
         }
     }
-    else if (fmt == IPP_TAPS_MFMA && dbg == 1)
-        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
-    else if (fmt == IPP_TAPS_MFMA && dbg == 2)
-        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 2>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
-    else if (fmt == IPP_TAPS_MFMA && dbg == 3)
-        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 3>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
-    else if (fmt == IPP_TAPS_MFMA && dbg == 4)
-        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 4>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
-    else if (fmt == IPP_TAPS_MFMA && dbg == 7)
-        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1, 7>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
-    else if (fmt == IPP_TAPS_MFMA)
-        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
-    else
-        hipLaunchKernelGGL((k_pipe_hpass<NR, ZONES, CN, 0>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp);
+#endif
+    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0);
 }
 
 template <int NR>
 void launch_hpass_nr(bool zones, int cn, dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp,
-                     const int32_t* coefs, const ipp_pipe_desc* descs, int fmt, int ty, const ipp_hsv_params& hp,
+                     const int32_t* coefs, const ipp_pipe_desc* descs, int ty, const ipp_hsv_params& hp,
                      const uint8_t* bg, uint8_t* dst) {
     if (zones) {
-        if (cn == 4) launch_hpass<NR, true, 4>(grid, s, src, tmp, coefs, descs, fmt, ty, hp, bg, dst);
-        else launch_hpass<NR, true, 3>(grid, s, src, tmp, coefs, descs, fmt, ty, hp, bg, dst);
+        if (cn == 4) launch_hpass<NR, true, 4>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst);
+        else launch_hpass<NR, true, 3>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst);
     } else {
-        if (cn == 4) launch_hpass<NR, false, 4>(grid, s, src, tmp, coefs, descs, fmt, ty, hp, bg, dst);
-        else launch_hpass<NR, false, 3>(grid, s, src, tmp, coefs, descs, fmt, ty, hp, bg, dst);
+        if (cn == 4) launch_hpass<NR, false, 4>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst);
+        else launch_hpass<NR, false, 3>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst);
     }
 }
 
 }  // namespace
-
-#ifdef IPP_DBG_DUMP
-extern "C" int ipp_dbg_dump(void* win, void* meta) {
-    hipMemcpyFromSymbol(win, HIP_SYMBOL(g_dbg_win), sizeof(g_dbg_win));
-    hipMemcpyFromSymbol(meta, HIP_SYMBOL(g_dbg_meta), sizeof(g_dbg_meta));
-    return 0;
-}
-#endif
 
 static int pipe_hpass_impl(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
                            int32_t n_images, int32_t max_out_w, int32_t max_rows, int32_t src_cn,
@@ -1018,8 +681,8 @@ static int pipe_hpass_impl(const uint8_t* src, uint8_t* tmp, const int32_t* coef
     if (n_images == 0) return IPP_OK;
     if (!src || !tmp || !coefs || !descs || !hsv || n_images < 0 || max_out_w <= 0 || max_rows <= 0) return IPP_E_ARG;
     if (src_cn != 3 && src_cn != 4) return IPP_E_ARG;
-    if (tap_format != IPP_TAPS_DOT4 && tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;
-    const int fmt = tap_format, ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
+    if (tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;  // the VALU dot4 kernels were retired
+    const int ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
     const int64_t blocks = (int64_t)ty * n_images;
     if ((int64_t)(ty + (bg ? copy_blocks_per_item() : 0)) * n_images >= INT32_MAX) return IPP_E_ARG;
     const dim3 grid((uint32_t)blocks);
@@ -1033,21 +696,21 @@ static int pipe_hpass_impl(const uint8_t* src, uint8_t* tmp, const int32_t* coef
     // A range that never matches: lo_v = 1 > hi_v = 0 (cv::inRange's empty range).
     const ipp_hsv_range never = ipp_hsv_range{{0, 0, 1}, {180, 255, 0}, {0, 0, 0, 0}};
     switch (hsv->n_ranges) {
-        case 1: launch_hpass_nr<1>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv, bg, dst); break;
-        case 2: launch_hpass_nr<2>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv, bg, dst); break;
-        case 3: launch_hpass_nr<3>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv, bg, dst); break;
-        case 4: launch_hpass_nr<4>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, *hsv, bg, dst); break;
+        case 1: launch_hpass_nr<1>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst); break;
+        case 2: launch_hpass_nr<2>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst); break;
+        case 3: launch_hpass_nr<3>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst); break;
+        case 4: launch_hpass_nr<4>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst); break;
         case 5: case 6: {
             ipp_hsv_params q = *hsv;  // pad with never-matching ranges (lo > hi in v)
             for (int k = q.n_ranges; k < 6; ++k) q.r[k] = never;
-            launch_hpass_nr<6>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, q, bg, dst);
+            launch_hpass_nr<6>(zones, cn, grid, s, src, tmp, coefs, descs, ty, q, bg, dst);
             break;
         }
         default: {
             if (hsv->n_ranges > IPP_MAX_HSV_RANGES) return IPP_E_ARG;
             ipp_hsv_params q = *hsv;
             for (int k = q.n_ranges; k < IPP_MAX_HSV_RANGES; ++k) q.r[k] = never;
-            launch_hpass_nr<IPP_MAX_HSV_RANGES>(zones, cn, grid, s, src, tmp, coefs, descs, fmt, ty, q, bg, dst);
+            launch_hpass_nr<IPP_MAX_HSV_RANGES>(zones, cn, grid, s, src, tmp, coefs, descs, ty, q, bg, dst);
             break;
         }
     }
@@ -1070,6 +733,19 @@ extern "C" int ipp_pipe_hpass_bgcopy(const uint8_t* src, uint8_t* tmp, const int
     if (!bg || !dst || tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;
     return pipe_hpass_impl(src, tmp, coefs, descs, n_images, max_out_w, max_rows, src_cn, hsv, tap_format, bg, dst,
                            stream);
+}
+
+extern "C" int ipp_pipe_status(int32_t* status, void* stream) {
+    if (!status) return IPP_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    const int32_t zero = 0;
+    if (hipMemcpyFromSymbolAsync(status, HIP_SYMBOL(g_pipe_status), sizeof(int32_t), 0, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipMemcpyToSymbolAsync(HIP_SYMBOL(g_pipe_status), &zero, sizeof(int32_t), 0, hipMemcpyHostToDevice, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return IPP_E_LAUNCH;
+    return IPP_OK;
 }
 
 extern "C" int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst, const int32_t* coefs,
@@ -1095,53 +771,29 @@ extern "C" int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* d
                                int32_t max_ov_w, int32_t tap_format, void* stream) {
     if (n_images == 0) return IPP_OK;
     if (!tmp || !bg || !dst || !coefs || !descs || n_images < 0 || bg_w <= 0 || bg_h <= 0) return IPP_E_ARG;
-    if (tap_format == IPP_TAPS_MFMA) {
-        if (max_ov_w <= 0 || max_ov_w > bg_w) return IPP_E_ARG;
-        const size_t sm = (size_t)VBR * max_ov_w * sizeof(uint32_t);
-        const int tyb = (bg_h + VBR - 1) / VBR;
-        const int64_t nb = (int64_t)tyb * n_images;
-        if (nb >= INT32_MAX || sm > 64 * 1024) return IPP_E_ARG;
-        const dim3 grid((uint32_t)nb);
-        hipStream_t st = (hipStream_t)stream;
-        static const int pol = [] {
-            const char* e = getenv("IPP_VB_STORE");
-            return e ? atoi(e) : 2;
-        }();
-        if (pol == 0)
-            hipLaunchKernelGGL(k_pipe_vblend_mfma<0>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
-        else if (pol == 1)
-            hipLaunchKernelGGL(k_pipe_vblend_mfma<1>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
-        else if (pol == 9)  // diagnostics (wrong output): no background reads
-            hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 1>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
-        else if (pol == 10)  // ... no V pass
-            hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 2>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
-        else if (pol == 11)  // ... stores only
-            hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 3>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
-        else
-            hipLaunchKernelGGL(k_pipe_vblend_mfma<2>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
-        IPP_CHECK_LAUNCH();
-        return IPP_OK;
+    if (tap_format != IPP_TAPS_MFMA || max_ov_w <= 0 || max_ov_w > bg_w) return IPP_E_ARG;
+    const size_t sm = (size_t)VBR * max_ov_w * sizeof(uint32_t);
+    const int tyb = (bg_h + VBR - 1) / VBR;
+    const int64_t nb = (int64_t)tyb * n_images;
+    if (nb >= INT32_MAX || sm > 64 * 1024) return IPP_E_ARG;
+    const dim3 grid((uint32_t)nb);
+    hipStream_t st = (hipStream_t)stream;
+#ifdef IPP_DIAG
+    // store policy 0 plain / 1 sc1 / 2 nt; experiment kernels (WRONG output):
+    // 9 no background reads, 10 no V pass, 11 stores only
+    static const int pol = diag_env("IPP_VB_STORE", 2);
+    switch (pol) {
+        case 0: hipLaunchKernelGGL(k_pipe_vblend_mfma<0>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        case 1: hipLaunchKernelGGL(k_pipe_vblend_mfma<1>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        case 9: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 1>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        case 10: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 2>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        case 11: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 3>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        default: hipLaunchKernelGGL(k_pipe_vblend_mfma<2>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
     }
-    if (tap_format != IPP_TAPS_DOT4) return IPP_E_ARG;
-    const size_t shmem = (size_t)VR * bg_w * sizeof(uint32_t);
-    if (shmem > 160 * 1024) return IPP_E_ARG;
-    const int ty = (bg_h + VR - 1) / VR;
-    const int64_t blocks = (int64_t)ty * n_images;
-    if (blocks >= INT32_MAX) return IPP_E_ARG;
-    // Composite store policy (IPP_VB_STORE = 0 plain, 1 sc1, 2 nt; default nt:
-    // the write-once output then does not evict the shared backgrounds).
-    static const int policy = [] {
-        const char* e = getenv("IPP_VB_STORE");
-        return e ? atoi(e) : 2;
-    }();
-    const dim3 grid((uint32_t)blocks);
-    hipStream_t s = (hipStream_t)stream;
-    if (policy == 0)
-        hipLaunchKernelGGL(k_pipe_vblend<0>, grid, dim3(256), shmem, s, tmp, bg, dst, coefs, descs, ty, bg_w);
-    else if (policy == 2)
-        hipLaunchKernelGGL(k_pipe_vblend<2>, grid, dim3(256), shmem, s, tmp, bg, dst, coefs, descs, ty, bg_w);
-    else
-        hipLaunchKernelGGL(k_pipe_vblend<1>, grid, dim3(256), shmem, s, tmp, bg, dst, coefs, descs, ty, bg_w);
+#else
+    // nt stores: the write-once composite does not evict the shared backgrounds
+    hipLaunchKernelGGL(k_pipe_vblend_mfma<2>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
+#endif
     IPP_CHECK_LAUNCH();
     return IPP_OK;
 }

@@ -18,7 +18,6 @@ device work is two launches for the whole batch (``ipp_pipe_hpass``,
 from __future__ import annotations
 
 import math
-import os
 import random
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
@@ -31,8 +30,6 @@ from . import geometry as G
 from .device import SYM_FLIP, _stream, _to_dev
 
 ALL_SYMS = ("o", "h", "v", "hv")
-# H-pass tap format: "mfma" (v_mfma_i32_16x16x64_i8 tiles) or "dot4" (VALU)
-TAPS = os.environ.get("IPP_TAPS", "mfma")
 H_RING_COLUMNS = 512   # ipp_pipe.hip RING
 
 
@@ -74,7 +71,7 @@ class PipePlan:
     bg_h: int
     algo_bytes_hpass: int = 0
     algo_bytes_vblend: int = 0
-    tap_format: int = 0                   # IPP_TAPS_DOT4 / IPP_TAPS_MFMA (H and V passes)
+    tap_format: int = 1                   # IPP_TAPS_MFMA (the only device format)
     max_ov_w: int = 1
     max_ov_h: int = 1
     # split form (ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands): the
@@ -83,18 +80,54 @@ class PipePlan:
     algo_bytes_vblend_bands: int = 0
 
 
-def draw_params(n: int, src_hw: Tuple[int, int], bg_hw: Tuple[int, int], n_bg: int, cfg: PipeConfig,
-                seed: int) -> Tuple[List[ItemParams], List[Tuple]]:
-    """Per-item random parameters in the reference's draw order.
+def draw_params(n_global: int, stop: int, src_hw: Tuple[int, int], bg_hw: Tuple[int, int], n_bg: int,
+                cfg: PipeConfig, seed: int):
+    """Every random draw of the 5-step pipeline, consumed from ONE stream in
+    the order a chained ``ProcessingPipeline`` of the five reference steps
+    consumes it (step-major: each step runs over all its files, in sorted
+    order, before the next step starts; pipeline.py:555-566):
 
-    pipeline.py:202 shuffles the background list once ('modulo' pairing);
-    per item: rotations.py:89 uniform, symmetry.py:122 sample(pool, 1),
-    overlays.py:108 uniform, :133-134 randint × 2.  The draws that depend on
-    geometry (positions) are resolved during planning (see plan_pipe)."""
+      1. crop_from_border          — no draw;
+      2. process_rotations         — one ``uniform(angle_min, angle_max)`` per
+                                     file (rotations.py:89; num_rotations=1,
+                                     include_original=False), all n_global files;
+      3. generate_symmetries       — one ``sample(pool, 1)`` per file
+                                     (symmetry.py:122; choose_random=1,
+                                     include_original=False), all n_global files;
+      4. process_images_with_color_masks — no draw;
+      5. paste_overlay_onto_background, 'modulo' pairing — ``shuffle`` of the
+         background list (pipeline.py:202), then per item ``uniform`` ratio
+         (overlays.py:108) and two ``randint`` (overlays.py:133-134), whose
+         ranges depend on the item's geometry, for items 0 .. stop-1.
+
+    Returns (angles, syms, order, per-item (ratio, x, y, geometry)) for
+    items 0 .. stop-1; items ≥ stop only consume their steps-2/3 draws."""
+    H, W = src_hw
+    bh, bw = bg_hw
     rng = random.Random(seed)
+    pool = list(cfg.sym_pool)
+    angles = [rng.uniform(cfg.angle_min, cfg.angle_max) for _ in range(n_global)]
+    syms = [rng.sample(pool, 1)[0] for _ in range(n_global)]
     order = list(range(n_bg))
     rng.shuffle(order)
-    return rng, order
+    t, b, l, r = G.crop_margins(H, W, cfg.margins)
+    wc, hc = W - l - r, H - t - b
+    per_item = []
+    for gi in range(stop):
+        plan = G.rotation_plan(wc, hc, angles[gi])
+        bb = G.rotated_bbox(wc, hc, plan)
+        if bb is not None and bb[2] > bb[0] and bb[3] > bb[1]:
+            box = (bb[0], bb[1], bb[2] - bb[0], bb[3] - bb[1])
+        else:
+            box = (0, 0, plan.nw, plan.nh)
+        ratio = rng.uniform(cfg.scale_min, cfg.scale_max)
+        nw_, nh_ = G.overlay_size(box[2], box[3], bw, bh, ratio)
+        if nw_ <= 0 or nh_ <= 0:
+            raise ValueError(f"item {gi}: degenerate overlay size {nw_}x{nh_}")
+        x = rng.randint(0, bw - nw_)
+        y = rng.randint(0, bh - nh_)
+        per_item.append((ratio, x, y, plan, box, (nw_, nh_)))
+    return angles, syms, order, per_item
 
 
 def shard_range(n_global: int, rank: int, world: int) -> Tuple[int, int]:
@@ -108,19 +141,25 @@ def shard_range(n_global: int, rank: int, world: int) -> Tuple[int, int]:
 
 
 def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int, cfg: PipeConfig,
-              seed: int = 0, src_pitch: Optional[int] = None, item_range: Optional[Tuple[int, int]] = None
-              ) -> PipePlan:
-    """Plan `n` items.  With ``item_range=(start, stop)`` the random stream is
-    drawn for the global items 0..stop-1 in the reference's order and only
-    items [start, stop) are planned (stop - start must equal n): every rank of
-    a sharded run sees exactly the parameters a single process would give
-    those items, so outputs do not depend on the number of GPUs."""
+              seed: int = 0, src_pitch: Optional[int] = None, item_range: Optional[Tuple[int, int]] = None,
+              n_global: Optional[int] = None) -> PipePlan:
+    """Plan `n` items.  The random stream is the one a chained file-mode
+    ``ProcessingPipeline`` of the five reference steps over ``n_global``
+    sources would consume under ``random.seed(seed)`` (``draw_params``).
+    With ``item_range=(start, stop)`` only items [start, stop) of that global
+    batch are planned (stop - start must equal n): every rank of a sharded run
+    sees exactly the parameters a single process would give those items, so
+    outputs do not depend on the number of GPUs.  ``n_global`` defaults to
+    ``stop``."""
     H, W = src_hw
     bh, bw = bg_hw
     start, stop = item_range if item_range is not None else (0, n)
     if stop - start != n or start < 0:
         raise ValueError(f"item_range {item_range} does not hold {n} items")
-    rng, order = draw_params(stop, src_hw, bg_hw, n_bg, cfg, seed)
+    n_global = stop if n_global is None else n_global
+    if n_global < stop:
+        raise ValueError(f"n_global {n_global} < item_range stop {stop}")
+    angles, syms, order, drawn = draw_params(n_global, stop, src_hw, bg_hw, n_bg, cfg, seed)
     t, b, l, r = G.crop_margins(H, W, cfg.margins)
     wc, hc = W - l - r, H - t - b
     d = np.zeros(n, N.PIPE_DESC)
@@ -128,24 +167,9 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     cut_dims, ov_dims = [], []
     # axis list for the batch tap planner: (in, out) pairs, H then V per item
     axes_in, axes_out, identity = [], [], []
-    pool = list(cfg.sym_pool)
-    for gi in range(stop):
-        angle = rng.uniform(cfg.angle_min, cfg.angle_max)
-        sym = rng.sample(pool, 1)[0]
-        plan = G.rotation_plan(wc, hc, angle)
-        bb = G.rotated_bbox(wc, hc, plan)
-        if bb is not None and bb[2] > bb[0] and bb[3] > bb[1]:
-            ox, oy, rw, rh = bb[0], bb[1], bb[2] - bb[0], bb[3] - bb[1]
-        else:
-            ox, oy, rw, rh = 0, 0, plan.nw, plan.nh
-        ratio = rng.uniform(cfg.scale_min, cfg.scale_max)
-        nw_, nh_ = G.overlay_size(rw, rh, bw, bh, ratio)
-        if nw_ <= 0 or nh_ <= 0:
-            raise ValueError(f"item {gi}: degenerate overlay size {nw_}x{nh_}")
-        x = rng.randint(0, bw - nw_)
-        y = rng.randint(0, bh - nh_)
-        if gi < start:
-            continue
+    for gi in range(start, stop):
+        ratio, x, y, plan, (ox, oy, rw, rh), (nw_, nh_) = drawn[gi]
+        angle, sym = angles[gi], syms[gi]
         i = gi - start
         params.append(ItemParams(angle, sym, order[gi % n_bg], ratio, x, y))
         cut_dims.append((rh, rw))
@@ -166,7 +190,7 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
         axes_in += [rw, rh]
         axes_out += [nw_, nh_]
 
-    # ---- taps (C planner, threaded; dot4 format, see ipp_host.cpp) --------
+    # ---- taps (C planner, threaded; MFMA tile format, see ipp_host.cpp) -----
     lib = N.load()
     m = 2 * n
     a_in = np.asarray(axes_in, np.int32)
@@ -176,24 +200,20 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     shift = np.array([(j % 2 == 1) and not identity[j // 2][0] for j in range(m)], np.int32)
     ks = np.array([1 if ident[j] else lib.ipp_plan_lanczos_ksize(0.0, float(a_in[j]), int(a_out[j]))
                    for j in range(m)], np.int64)
-    ngs = np.array([lib.ipp_plan_dot4_stride(int(k)) for k in ks], np.int64)
-    mfma = TAPS == "mfma"
     # The H pass keeps each output tile's input window in a 512-column LDS ring
-    # (ipp_pipe.hip RING): 64·nK columns (mfma) or 4·ngs (dot4) must fit.
+    # (ipp_pipe.hip RING): 64·nK columns must fit.
     for j in range(0, m, 2):
         if ident[j]:
             continue
-        cols = (64 * lib.ipp_plan_mfma_nk_bound(int(a_in[j]), int(a_out[j]), int(ks[j])) if mfma
-                else 4 * int(ngs[j]))
+        cols = 64 * lib.ipp_plan_mfma_nk_bound(int(a_in[j]), int(a_out[j]), int(ks[j]))
         if cols > H_RING_COLUMNS:
             raise ValueError(f"item {j // 2}: LANCZOS downscale {a_in[j]} -> {a_out[j]} needs a {cols}-column "
                              f"window, more than the fused H pass holds ({H_RING_COLUMNS}); use the plugin path")
-    # H axes (even j): mfma tiles or transposed dot4; V axes: row-major dot4
-    # (V axes in mfma form: tiles aligned with 16-row background bands, phase = y mod 16)
-    transp = np.array([(2 if mfma else 1) if j % 2 == 0 else ((2 + params[j // 2].y % 16) if mfma else 0)
-                       for j in range(m)], np.int32)
-    sizes = np.array([lib.ipp_plan_mfma_size(int(a_in[j]), int(a_out[j]), int(ks[j])) if transp[j] >= 2
-                      else 4 * int(a_out[j]) * (1 + int(ngs[j])) for j in range(m)], np.int64)
+    # H axes (even j): tiles of 16 outputs; V axes: tiles aligned with 16-row
+    # background bands (phase = y mod 16)
+    transp = np.array([2 if j % 2 == 0 else 2 + params[j // 2].y % 16 for j in range(m)], np.int32)
+    sizes = np.array([lib.ipp_plan_mfma_size(int(a_in[j]), int(a_out[j]), int(ks[j])) for j in range(m)],
+                     np.int64)
     sizes = (sizes + 3) // 4 * 4          # 16-B aligned axis blocks
     offs = np.zeros(m, np.int64)
     offs[1:] = np.cumsum(sizes)[:-1]
@@ -216,21 +236,19 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
         else:
             y0, y1 = 0, rh
         rows = y1 - y0
-        if mfma:   # V tiles read up to 64·nK rows past their 16-aligned start
-            nkb = lib.ipp_plan_mfma_nk_bound(int(a_in[jv]), int(a_out[jv]), int(ks[jv]))
-            groups = (((rows + 15) // 16) * 16 + 64 * nkb + 16) // 4
-        else:
-            groups = ((rows + 15) // 16) * 4 + int(ngs[jv]) + 1   # + V-pass over-read pad
+        # V tiles read up to 64·nK rows past their 16-aligned start
+        nkb = lib.ipp_plan_mfma_nk_bound(int(a_in[jv]), int(a_out[jv]), int(ks[jv]))
+        groups = (((rows + 15) // 16) * 16 + 64 * nkb + 16) // 4
         pitch = 16 * nw_
         h = d[i]["h"]
         h["dst_off"] = tmp_off
         h["dst_pitch"] = pitch
-        h["in_len"], h["out_len"], h["lines"], h["line0"], h["ksize"] = rw, nw_, rows, y0, ngs[jh]
+        h["in_len"], h["out_len"], h["lines"], h["line0"], h["ksize"] = rw, nw_, rows, y0, ks[jh]
         h["coef_off"] = offs[jh]
         v = d[i]["v"]
         v["src_off"] = tmp_off
         v["src_pitch"] = pitch
-        v["in_len"], v["out_len"], v["lines"], v["ksize"] = rows, nh_, nw_, ngs[jv]
+        v["in_len"], v["out_len"], v["lines"], v["ksize"] = rows, nh_, nw_, ks[jv]
         v["coef_off"] = offs[jv]
         p = d[i]["p"]
         it = params[i]
@@ -257,7 +275,7 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     hsv = G.hsv_params(cfg.hsv_ranges, cfg.zones, cfg.use_gimp_scale, bgr=False)
     copy_bytes = 2 * 3 * bw * copy_rows           # read + write of the rows outside the bands
     return PipePlan(d, coefs, hsv, params, cut_dims, ov_dims, max(tmp_off, 256), max_out_w, max_rows, bw, bh,
-                    algo_h, algo_v, N.IPP_TAPS_MFMA if mfma else N.IPP_TAPS_DOT4,
+                    algo_h, algo_v, N.IPP_TAPS_MFMA,
                     max(w for _, w in ov_dims), max(h for h, _ in ov_dims),
                     algo_h + copy_bytes, algo_v - copy_bytes)
 
@@ -300,6 +318,13 @@ class PipeRunner:
                                                self.coefs.data_ptr(), self.descs.data_ptr(), len(p.descs), p.bg_w,
                                                p.bg_h, p.max_ov_w, p.max_ov_h, p.tap_format,
                                                _stream(self.device)), "ipp_pipe_vblend_bands")
+
+    def status(self) -> int:
+        """Sticky status of the pipe kernels since the last call (ipp_pipe_status;
+        bit 0: an H tile's window exceeded the LDS ring).  Synchronises."""
+        st = np.zeros(1, np.int32)
+        N.check(self.lib.ipp_pipe_status(N.np_ptr(st), _stream(self.device)), "ipp_pipe_status")
+        return int(st[0])
 
     @property
     def split(self) -> bool:

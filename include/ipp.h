@@ -187,7 +187,12 @@ typedef struct ipp_pipe_desc {
 #define IPP_TAPS_DOT4 0   /* per-output dot4 planes, v_dot4 on the VALU       */
 #define IPP_TAPS_MFMA 1   /* 16-output tiles, v_mfma_i32_16x16x64_i8          */
 
-/* src_cn: channels of every source in the batch (3 or 4); hsv: HOST pointer. */
+/* src_cn: channels of every source in the batch (3 or 4); hsv: HOST pointer.
+ * Ring limit: the H pass keeps each 16-output tile's input window in a
+ * 512-column LDS ring, so every H tile must satisfy 64·nK ≤ 512 (nK = its K
+ * steps; ipp_plan_mfma_nk_bound(in, out, ksize) ≤ 8, i.e. LANCZOS downscales
+ * of at most ≈ 23×; fused.plan_pipe refuses plans beyond it).  A violating tile sets bit 0 of the sticky status read by
+ * ipp_pipe_status; its T columns are then wrong. */
 int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                    const ipp_pipe_desc* descs, int32_t n_images,
                    int32_t max_out_w, int32_t max_rows, int32_t src_cn,
@@ -200,6 +205,10 @@ int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
                     const int32_t* coefs, const ipp_pipe_desc* descs, int32_t n_images,
                     int32_t bg_w, int32_t bg_h, int32_t max_ov_w, int32_t tap_format,
                     void* stream);
+
+/* Reads and clears the sticky status of the pipe kernels (bit 0: ring limit
+ * violated, see ipp_pipe_hpass).  Synchronises `stream`. */
+int ipp_pipe_status(int32_t* status, void* stream);
 
 /* Split form of the pair above (MFMA taps only), used by the batched device
  * mode (fused.PipeRunner.run).  A composite's rows outside the 16-row bands
@@ -317,6 +326,14 @@ int32_t ipp_plan_lanczos_ksize(double in0, double in1, int32_t out_size);
  * row with exact integer arithmetic.  bbox = (x0, y0, x1, y1) or all -1. */
 int ipp_plan_opaque_bbox(int32_t in_w, int32_t in_h, const int32_t a[6],
                          int32_t nw, int32_t nh, int32_t bbox[4]);
+
+/* ------------------------------------------------------------------------ */
+/* Measurement helper (the copy-kernel ceiling of the box).     */
+/* ------------------------------------------------------------------------ */
+/* dst[0, nbytes) = src[0, nbytes) with 16-B non-temporal loads/stores; both
+ * pointers 16-B aligned.  Not a reference call site: bench.py times it to
+ * report the roofline against the HBM rate a plain copy reaches here. */
+int ipp_stream_copy(const uint8_t* src, uint8_t* dst, int64_t nbytes, void* stream);
 
 /* Library version / build info string. */
 const char* ipp_version(void);

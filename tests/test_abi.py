@@ -75,3 +75,15 @@ def test_hsv_tables_in_source_match_cvround():
     from oracle.ops import SDIV_TABLE, HDIV_TABLE_180
     assert np.array_equal(table("kSdiv"), SDIV_TABLE)
     assert np.array_equal(table("kHdiv180"), HDIV_TABLE_180)
+
+
+def test_product_library_reads_no_environment():
+    """Diagnostic kernel switches exist only in -DIPP_DIAG builds: the product
+    libipp.so does not even import getenv, so no environment variable can
+    select a different (wrong-output) kernel."""
+    import subprocess
+    from image_processor_pipeline_amd import _native as N
+    nm = "/opt/rocm/lib/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "-D", "--undefined-only", str(N.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    assert "getenv" not in out and "secure_getenv" not in out

@@ -26,7 +26,8 @@ def _worker(rank, world, port, n_global, result_q):
     try:
         start, stop = fused.shard_range(n_global, rank, world)
         cfg = fused.PipeConfig(margins=(8, 8, 8, 8))
-        plan = fused.plan_pipe((96, 80), stop - start, (64, 72), 3, cfg, seed=5, item_range=(start, stop))
+        plan = fused.plan_pipe((96, 80), stop - start, (64, 72), 3, cfg, seed=5, item_range=(start, stop),
+                                n_global=n_global)
         bgs = torch.zeros((3, 64, 72, 3), dtype=torch.uint8)
         if rank == 0:
             bgs.copy_(torch.randint(0, 256, bgs.shape, dtype=torch.uint8, generator=torch.Generator().manual_seed(1)))
