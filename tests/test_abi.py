@@ -81,9 +81,10 @@ def test_product_library_reads_no_environment():
     """Diagnostic kernel switches exist only in -DIPP_DIAG builds: the product
     libipp.so does not even import getenv, so no environment variable can
     select a different (wrong-output) kernel."""
+    import shutil
     import subprocess
     from image_processor_pipeline_amd import _native as N
-    nm = "/opt/rocm/lib/llvm/bin/llvm-nm"
+    nm = shutil.which("nm") or "/usr/bin/nm"
     out = subprocess.run([nm, "-D", "--undefined-only", str(N.LIB_PATH)], capture_output=True, text=True,
                          check=True).stdout
     assert "getenv" not in out and "secure_getenv" not in out
