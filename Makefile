@@ -5,7 +5,7 @@ ARCH ?= gfx950
 PKG := image_processor_pipeline_amd
 CSRC := $(PKG)/csrc
 SRCS := $(CSRC)/ipp_gather.hip $(CSRC)/ipp_hsv.hip $(CSRC)/ipp_resample.hip $(CSRC)/ipp_pipe.hip \
-        $(CSRC)/ipp_ccl.hip $(CSRC)/ipp_util.hip
+        $(CSRC)/ipp_ccl.hip $(CSRC)/ipp_util.hip $(CSRC)/ipp_bilinear.hip
 HOST_SRCS := $(CSRC)/ipp_host.cpp
 HDRS := include/ipp.h $(wildcard $(CSRC)/*.h)
 OBJDIR := build/obj

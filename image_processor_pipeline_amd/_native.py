@@ -46,6 +46,12 @@ GATHER_DESC = np.dtype([
     ("out_w", _I4), ("out_h", _I4), ("off_x", _I4), ("off_y", _I4), ("flip", _I4), ("dst_pitch", _I4),
 ], align=True)
 
+AFFINE_DESC = np.dtype([
+    ("src_off", _I8), ("dst_off", _I8), ("src_pitch", _I4), ("src_cn", _I4),
+    ("in_x0", _I4), ("in_y0", _I4), ("in_w", _I4), ("in_h", _I4),
+    ("out_w", _I4), ("out_h", _I4), ("dst_pitch", _I4), ("flip", _I4), ("m", np.float64, (6,)),
+], align=True)
+
 COPY_DESC = np.dtype([
     ("src_off", _I8), ("dst_off", _I8), ("src_pitch", _I4), ("dst_pitch", _I4),
     ("x0", _I4), ("y0", _I4), ("w", _I4), ("h", _I4), ("cn", _I4), ("flip", _I4),
@@ -81,6 +87,7 @@ _L = ctypes.c_int64
 _D = ctypes.c_double
 SIGNATURES = {
     "ipp_rotate_flip_nearest": (_I, [_P, _P, _P, _I, _I, _I, _P]),
+    "ipp_rotate_bilinear": (_I, [_P, _P, _P, _I, _I, _I, _P]),
     "ipp_copy_window": (_I, [_P, _P, _P, _I, _I, _I, _P]),
     "ipp_crop_to_bbox": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ipp_hsv_mask": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),

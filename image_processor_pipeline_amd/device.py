@@ -145,6 +145,41 @@ def rotate_crop_single(img: torch.Tensor, angle: float, flip: int = 0) -> torch.
     return copy_window(canvas, (x0, y0, x1 - x0, y1 - y0), flip)
 
 
+def rotate_bilinear_canvas(img: torch.Tensor, angle: float, flip: int = 0) -> torch.Tensor:
+    """Pillow ``convert('RGBA').rotate(angle, expand=True, resample=BILINEAR)``
+    canvas of an RGB/RGBA image (ipp_rotate_bilinear; fast-path angles are
+    transposes and take the NEAREST gather), flip bits folded in."""
+    _require_cuda(img, "rotate_bilinear_canvas")
+    img = img.contiguous()
+    h, w, cn = img.shape
+    plan = G.rotation_plan(w, h, float(angle))
+    if plan.M is None:   # 0/90/180/270: exact transposes, identical for every filter
+        gp = plan_rotate_flip([(h, w, cn)], [angle], [flip], crop_to_bbox=False)
+        return unpack(rotate_flip_nearest(img.reshape(-1), gp), gp)[0].contiguous()
+    d = np.zeros(1, N.AFFINE_DESC)
+    d[0]["src_pitch"], d[0]["src_cn"] = w * cn, cn
+    d[0]["in_w"], d[0]["in_h"] = w, h
+    d[0]["out_w"], d[0]["out_h"], d[0]["dst_pitch"], d[0]["flip"] = plan.nw, plan.nh, 4 * plan.nw, flip
+    d[0]["m"] = plan.M
+    out = torch.empty((plan.nh, plan.nw, 4), dtype=torch.uint8, device=img.device)
+    dd = _to_dev(d, img.device)
+    N.check(N.load().ipp_rotate_bilinear(img.data_ptr(), out.data_ptr(), dd.data_ptr(), 1, plan.nw, plan.nh,
+                                         _stream(img.device)), "ipp_rotate_bilinear")
+    _keep(dd)
+    return out
+
+
+def rotate_crop_bilinear(img: torch.Tensor, angle: float, flip: int = 0) -> torch.Tensor:
+    """rotations.py:96-109 with resample=BILINEAR: canvas, then its alpha
+    bbox (fallback: the uncropped canvas when None or empty)."""
+    canvas = rotate_bilinear_canvas(img, angle, flip)
+    bb = alpha_bbox([canvas])[0]
+    if bb is None or bb[2] <= bb[0] or bb[3] <= bb[1]:
+        return canvas
+    x0, y0, x1, y1 = bb
+    return copy_window(canvas, (x0, y0, x1 - x0, y1 - y0))
+
+
 # ---------------------------------------------------------------------------
 # Window copy / flip (recadrages.py:46, crop_square.py:196, symmetry.py:114-119)
 # ---------------------------------------------------------------------------

@@ -114,20 +114,28 @@ def draw_params(n_global: int, stop: int, src_hw: Tuple[int, int], bg_hw: Tuple[
     wc, hc = W - l - r, H - t - b
     per_item = []
     for gi in range(stop):
-        plan = G.rotation_plan(wc, hc, angles[gi])
-        bb = G.rotated_bbox(wc, hc, plan)
-        if bb is not None and bb[2] > bb[0] and bb[3] > bb[1]:
-            box = (bb[0], bb[1], bb[2] - bb[0], bb[3] - bb[1])
-        else:
-            box = (0, 0, plan.nw, plan.nh)
         ratio = rng.uniform(cfg.scale_min, cfg.scale_max)
-        nw_, nh_ = G.overlay_size(box[2], box[3], bw, bh, ratio)
-        if nw_ <= 0 or nh_ <= 0:
-            raise ValueError(f"item {gi}: degenerate overlay size {nw_}x{nh_}")
+        plan, box, (nw_, nh_) = item_geometry(wc, hc, angles[gi], ratio, bw, bh, gi)
         x = rng.randint(0, bw - nw_)
         y = rng.randint(0, bh - nh_)
         per_item.append((ratio, x, y, plan, box, (nw_, nh_)))
     return angles, syms, order, per_item
+
+
+def item_geometry(wc: int, hc: int, angle: float, ratio: float, bw: int, bh: int, gi: int = 0):
+    """One item's host geometry: the rotation plan of the wc×hc crop
+    (rotations.py:96), its bbox (x, y, w, h) (rotations.py:99-109, fallback
+    to the whole canvas) and the resized overlay (w, h) (overlays.py:106-126)."""
+    plan = G.rotation_plan(wc, hc, angle)
+    bb = G.rotated_bbox(wc, hc, plan)
+    if bb is not None and bb[2] > bb[0] and bb[3] > bb[1]:
+        box = (bb[0], bb[1], bb[2] - bb[0], bb[3] - bb[1])
+    else:
+        box = (0, 0, plan.nw, plan.nh)
+    nw_, nh_ = G.overlay_size(box[2], box[3], bw, bh, ratio)
+    if nw_ <= 0 or nh_ <= 0:
+        raise ValueError(f"item {gi}: degenerate overlay size {nw_}x{nh_}")
+    return plan, box, (nw_, nh_)
 
 
 def shard_range(n_global: int, rank: int, world: int) -> Tuple[int, int]:
@@ -142,7 +150,7 @@ def shard_range(n_global: int, rank: int, world: int) -> Tuple[int, int]:
 
 def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int, cfg: PipeConfig,
               seed: int = 0, src_pitch: Optional[int] = None, item_range: Optional[Tuple[int, int]] = None,
-              n_global: Optional[int] = None) -> PipePlan:
+              n_global: Optional[int] = None, params: Optional[Sequence[ItemParams]] = None) -> PipePlan:
     """Plan `n` items.  The random stream is the one a chained file-mode
     ``ProcessingPipeline`` of the five reference steps over ``n_global``
     sources would consume under ``random.seed(seed)`` (``draw_params``).
@@ -150,7 +158,9 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     batch are planned (stop - start must equal n): every rank of a sharded run
     sees exactly the parameters a single process would give those items, so
     outputs do not depend on the number of GPUs.  ``n_global`` defaults to
-    ``stop``."""
+    ``stop``.  With ``params`` (one ItemParams per item) nothing is drawn:
+    the caller's angles, symmetries, backgrounds, ratios and positions are
+    planned as given (positions must keep the overlay inside the background)."""
     H, W = src_hw
     bh, bw = bg_hw
     start, stop = item_range if item_range is not None else (0, n)
@@ -159,19 +169,32 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     n_global = stop if n_global is None else n_global
     if n_global < stop:
         raise ValueError(f"n_global {n_global} < item_range stop {stop}")
-    angles, syms, order, drawn = draw_params(n_global, stop, src_hw, bg_hw, n_bg, cfg, seed)
     t, b, l, r = G.crop_margins(H, W, cfg.margins)
     wc, hc = W - l - r, H - t - b
+    if params is None:
+        angles, syms, order, drawn = draw_params(n_global, stop, src_hw, bg_hw, n_bg, cfg, seed)
+        given = None
+    else:
+        if len(params) != n:
+            raise ValueError(f"{len(params)} ItemParams for {n} items")
+        given = list(params)
     d = np.zeros(n, N.PIPE_DESC)
     params: List[ItemParams] = []
     cut_dims, ov_dims = [], []
     # axis list for the batch tap planner: (in, out) pairs, H then V per item
     axes_in, axes_out, identity = [], [], []
     for gi in range(start, stop):
-        ratio, x, y, plan, (ox, oy, rw, rh), (nw_, nh_) = drawn[gi]
-        angle, sym = angles[gi], syms[gi]
         i = gi - start
-        params.append(ItemParams(angle, sym, order[gi % n_bg], ratio, x, y))
+        if given is None:
+            ratio, x, y, plan, (ox, oy, rw, rh), (nw_, nh_) = drawn[gi]
+            angle, sym, bgi = angles[gi], syms[gi], order[gi % n_bg]
+        else:
+            it = given[i]
+            angle, sym, bgi, ratio, x, y = it.angle, it.sym, it.bg_index, it.ratio, it.x, it.y
+            plan, (ox, oy, rw, rh), (nw_, nh_) = item_geometry(wc, hc, angle, ratio, bw, bh, gi)
+            if not (0 <= x <= bw - nw_ and 0 <= y <= bh - nh_ and 0 <= bgi < n_bg and sym in SYM_FLIP):
+                raise ValueError(f"item {gi}: parameters {it} do not fit a {bw}x{bh} background")
+        params.append(ItemParams(angle, sym, bgi, ratio, x, y))
         cut_dims.append((rh, rw))
         ov_dims.append((nh_, nw_))
         g = d[i]["g"]

@@ -38,6 +38,11 @@ class RotationPlan:
     nw: int              # canvas width  (expand=True)
     nh: int              # canvas height
     A: Tuple[int, int, int, int, int, int]  # 16.16 inverse map (a0..a5)
+    M: Optional[Tuple[float, ...]] = None   # Pillow's double matrix ('affine' / 'scale_affine'; BILINEAR)
+
+
+def _with_m(plan: "RotationPlan", m) -> "RotationPlan":
+    return RotationPlan(plan.kind, plan.nw, plan.nh, plan.A, tuple(m))
 
 
 def _fix(v: float) -> int:
@@ -72,13 +77,13 @@ def rotation_plan(w: int, h: int, angle: float) -> RotationPlan:
     nh = math.ceil(max(ys)) - math.floor(min(ys))
     m[2], m[5] = tr(-(nw - w) / 2.0, -(nh - h) / 2.0)
     if m[1] == 0 and m[3] == 0:
-        return _scale_affine_plan(w, h, nw, nh, m)
+        return _with_m(_scale_affine_plan(w, h, nw, nh, m), m)
     for x, y in ((0, 0), (nw, nh), (0, nh), (nw, 0)):
         if not (abs(x * m[0] + y * m[1] + m[2]) < 32768.0 and abs(x * m[3] + y * m[4] + m[5]) < 32768.0):
             raise NotImplementedError("rotation canvas beyond Pillow's 16.16 fixed-point range (>32767 px)")
     A = (_fix(m[0]), _fix(m[1]), _fix(m[2] + m[0] * 0.5 + m[1] * 0.5),
          _fix(m[3]), _fix(m[4]), _fix(m[5] + m[3] * 0.5 + m[4] * 0.5))
-    return RotationPlan("affine", nw, nh, A)
+    return RotationPlan("affine", nw, nh, A, tuple(m))
 
 
 def _scale_affine_plan(w, h, nw, nh, m) -> RotationPlan:

@@ -21,9 +21,22 @@ from .. import _rt
 from .. import device as D
 
 
-def _rotate(img_dev, opaque: bool, angle: float, name: str, idx: int) -> np.ndarray:
+def _rotate(img_dev, opaque: bool, angle: float, name: str, idx: int, resample: str = "nearest") -> np.ndarray:
     """rotations.py:96-109 with its two fallbacks (None / empty bbox)."""
     h, w, _ = img_dev.shape
+    if resample == "bilinear":
+        canvas = D.rotate_bilinear_canvas(img_dev, angle)
+        bb = D.alpha_bbox([canvas])[0]
+        if bb is None:
+            print(f"Avertissement [{name} - Rotation]: Impossible d'obtenir BBox après rotation {idx}. "
+                  "Utilisation de l'image non recadrée.")
+            return _rt.d2h(canvas)
+        x0, y0, x1, y1 = bb
+        if x1 - x0 <= 0 or y1 - y0 <= 0:
+            print(f"Avertissement [{name} - Rotation]: Recadrage après rotation {idx} vide. "
+                  "Utilisation de l'image non recadrée.")
+            return _rt.d2h(canvas)
+        return _rt.d2h(D.copy_window(canvas, (x0, y0, x1 - x0, y1 - y0)))
     if opaque:
         plan = D.plan_rotate_flip([(h, w, img_dev.shape[2])], [angle], [0])
         return _rt.d2h(D.unpack(D.rotate_flip_nearest(img_dev.reshape(-1), plan), plan)[0])
@@ -54,8 +67,14 @@ def process_rotations(
     output_prefix: str = "r",
     original_key: str = "r000",
     rotation_key_format: str = "{prefix}{index:03d}",
+    resample: str = "nearest",
     **options: Any,
 ) -> Optional[List[Path]]:
+    """``resample`` (not in the reference, whose rotate is NEAREST): "nearest"
+    (default, bit-exact with rotations.py:96) or "bilinear" (opt-in, bit-exact
+    with Pillow ``rotate(..., resample=BILINEAR)``)."""
+    if resample not in ("nearest", "bilinear"):
+        raise ValueError(f"resample must be 'nearest' or 'bilinear', not {resample!r}")
     if not output_dirs:
         print(f"Erreur [{input_path.name} - Rotation]: Aucun dossier de sortie ('output_paths') fourni.")
         return None
@@ -95,7 +114,7 @@ def process_rotations(
     for i in range(num_rotations):
         angle = random.uniform(angle_min, angle_max)
         try:
-            rotated = _rotate(img_dev, not has_alpha, angle, input_path.name, i + 1)
+            rotated = _rotate(img_dev, not has_alpha, angle, input_path.name, i + 1, resample)
             key = rotation_key_format.format(prefix=output_prefix, index=i + 1)
             p = target_dir / f"{base_name}_{key}{out_suffix}"
             Image.fromarray(rotated, "RGBA").save(p, format=output_format)
@@ -113,7 +132,8 @@ def process_rotations(
 def _rotations_batch(arg_tuples, output_dirs: List[Path], threads: int = 1, num_rotations: int = 10,
                      include_original: bool = True, angle_min: float = 1.0, angle_max: float = 359.0,
                      output_format: str = "png", output_prefix: str = "r", original_key: str = "r000",
-                     rotation_key_format: str = "{prefix}{index:03d}", **options: Any) -> List:
+                     rotation_key_format: str = "{prefix}{index:03d}", resample: str = "nearest",
+                     **options: Any) -> List:
     """Batched process_rotations for ProcessingStep (one result per input).
 
     Decode on `threads` host threads; draw the angles in the sequential
@@ -121,8 +141,13 @@ def _rotations_batch(arg_tuples, output_dirs: List[Path], threads: int = 1, num_
     calls); all opaque sources of the chunk go through ONE fused gather
     launch (rotate + analytic bbox crop); alpha sources use the per-file
     device path; encode on host threads."""
-    if not output_dirs:
-        return [process_rotations(*a, output_dirs=output_dirs) for a in arg_tuples]
+    if not output_dirs or resample != "nearest":
+        # per-file path (the bilinear mode has no batched gather)
+        return [process_rotations(*a, output_dirs=output_dirs, num_rotations=num_rotations,
+                                  include_original=include_original, angle_min=angle_min, angle_max=angle_max,
+                                  output_format=output_format, output_prefix=output_prefix,
+                                  original_key=original_key, rotation_key_format=rotation_key_format,
+                                  resample=resample, **options) for a in arg_tuples]
     target_dir = Path(output_dirs[0])
     fmt = output_format.lower()
     out_suffix = ".jpg" if fmt == "jpeg" else f".{fmt}"

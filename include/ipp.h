@@ -70,6 +70,27 @@ int ipp_rotate_flip_nearest(const uint8_t* src, uint8_t* dst,
                             const ipp_gather_desc* descs, int32_t n_images,
                             int32_t max_out_w, int32_t max_out_h, void* stream);
 
+/* Opt-in BILINEAR rotation: Pillow rotate(angle, expand=True,
+ * resample=BILINEAR) of an RGB/RGBA source through RGBa (PIL/Image.py:2978-
+ * 2983, Geometry.c affine_transform + bilinear_filter32RGB).  The
+ * reference's rotations.py:96 is NEAREST; north_star asks for "rotations.py
+ * (bilinear)" — process_rotations(..., resample="bilinear").  Output: the
+ * full RGBA canvas (out_w × out_h = the expanded size) with the flip bits
+ * folded into the write (bit0 mirror x, bit1 mirror y); the caller crops it
+ * to its alpha bbox (ipp_alpha_bbox + ipp_copy_window).  m = Pillow's double
+ * inverse matrix. */
+typedef struct ipp_affine_desc {
+    int64_t src_off, dst_off;
+    int32_t src_pitch, src_cn;        /* cn 3 (α = 255) or 4 (RGBA)          */
+    int32_t in_x0, in_y0, in_w, in_h; /* source window seen by rotate        */
+    int32_t out_w, out_h, dst_pitch;  /* canvas; dst_pitch multiple of 4     */
+    int32_t flip;
+    double m[6];
+} ipp_affine_desc;
+
+int ipp_rotate_bilinear(const uint8_t* src, uint8_t* dst, const ipp_affine_desc* descs,
+                        int32_t n_images, int32_t max_out_w, int32_t max_out_h, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* Plain 2-D window copy / flip (recadrages.py:46 slice, crop_square.py:196  */
 /* slice, symmetry.py:114-119 cv2.flip codes 1/0/-1, pixels_isolés.py:81).   */

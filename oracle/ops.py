@@ -93,6 +93,42 @@ def rotate_expand_nearest(img: np.ndarray, angle: float) -> np.ndarray:
     return out
 
 
+def rotate_expand_bilinear(img: np.ndarray, angle: float) -> np.ndarray:
+    """Pillow ``img.rotate(angle, expand=True, resample=BILINEAR)`` for an RGBA
+    array — the opt-in BILINEAR mode of process_rotations (north_star names
+    "rotations.py (bilinear)"; the reference's own call, rotations.py:96, is
+    NEAREST).  PIL/Image.py:2978-2983 runs RGBA through RGBa; Geometry.c
+    ``affine_transform`` maps output (x, y) to ``a0(x+.5) + a1(y+.5) + a2``
+    in double and ``bilinear_filter32RGB`` rejects points outside [0, w) ×
+    [0, h), shifts by -0.5, clamps the x neighbours and the first row, falls
+    back to row y when y+1 is out of range, lerps in double and truncates
+    (SURVEY Appendix A9).  The 0/90/180/270 fast paths are transposes."""
+    h, w = img.shape[:2]
+    g = rotate_geometry(w, h, angle)
+    if g["kind"] in ("copy", "rot90", "rot180", "rot270"):
+        return rotate_expand_nearest(img, angle)
+    m0, m1, m2, m3, m4, m5 = g["matrix"]
+    nw, nh = g["nw"], g["nh"]
+    src = premultiply(img).astype(np.float64)
+    X = np.arange(nw, dtype=np.float64)[None, :] + 0.5
+    Y = np.arange(nh, dtype=np.float64)[:, None] + 0.5
+    xin = m0 * X + m1 * Y + m2
+    yin = m3 * X + m4 * Y + m5
+    ok = (xin >= 0.0) & (xin < w) & (yin >= 0.0) & (yin < h)
+    xs, ys = xin - 0.5, yin - 0.5
+    xi, yi = np.floor(xs), np.floor(ys)
+    dx, dy = (xs - xi)[..., None], (ys - yi)[..., None]
+    xi, yi = xi.astype(np.int64), yi.astype(np.int64)
+    x0, x1 = np.clip(xi, 0, w - 1), np.clip(xi + 1, 0, w - 1)
+    y0, y1 = np.clip(yi, 0, h - 1), np.clip(yi + 1, 0, h - 1)
+    y1ok = ((yi + 1 >= 0) & (yi + 1 < h))[..., None]
+    v1 = src[y0, x0] + (src[y0, x1] - src[y0, x0]) * dx
+    v2 = np.where(y1ok, src[y1, x0] + (src[y1, x1] - src[y1, x0]) * dx, v1)
+    v = v1 + (v2 - v1) * dy
+    out = np.where(ok[..., None], v, 0.0).astype(np.uint8)
+    return unpremultiply(out)
+
+
 def getbbox_alpha(img: np.ndarray) -> Optional[Tuple[int, int, int, int]]:
     """Pillow ``getbbox()`` (alpha_only=True) on an RGBA array.
 
@@ -110,10 +146,10 @@ def getbbox_alpha(img: np.ndarray) -> Optional[Tuple[int, int, int, int]]:
     return int(cols[0]), int(rows[0]), int(cols[-1]) + 1, int(rows[-1]) + 1
 
 
-def rotate_and_crop(img_rgba: np.ndarray, angle: float) -> np.ndarray:
+def rotate_and_crop(img_rgba: np.ndarray, angle: float, resample: str = "nearest") -> np.ndarray:
     """rotations.py:96-109: rotate, then crop to the alpha bbox (fallback:
     the uncropped canvas when the bbox is None or empty)."""
-    rot = rotate_expand_nearest(img_rgba, angle)
+    rot = (rotate_expand_bilinear if resample == "bilinear" else rotate_expand_nearest)(img_rgba, angle)
     bb = getbbox_alpha(rot)
     if bb is None:
         return rot

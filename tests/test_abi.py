@@ -40,6 +40,7 @@ STRUCTS = {
     "ipp_paste_desc": N.PASTE_DESC,
     "ipp_pipe_desc": N.PIPE_DESC,
     "ipp_ccl_work": N.CCL_WORK,
+    "ipp_affine_desc": N.AFFINE_DESC,
 }
 
 

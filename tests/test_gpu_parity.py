@@ -372,3 +372,52 @@ def test_crop_to_bbox_and_vector_copy(D):
     assert np.array_equal(out[0, :26, :37], imgs[0, 4:30, 3:40])
     assert not out[1].any()
     assert np.array_equal(out[2], imgs[2])
+
+
+# --------------------------------------------------------------------------- round 2: Pillow pins at real geometry
+
+def test_rotate_bilinear_matches_pillow_goldens(D, golden):
+    """Opt-in BILINEAR rotate (ipp_rotate_bilinear, fp64 as Pillow): canvases
+    bit-exact with Pillow, bbox crops too, flips folded into the write."""
+    g = golden("rotate_bilinear_pillow.npz")
+    srcs = unpack(g["src_flat"], g["src_shapes"])
+    outs = unpack(g["out_flat"], g["out_shapes"])
+    for k, (out, si, a, bb) in enumerate(zip(outs, g["src_index"], g["angles"], g["bboxes"])):
+        fl = k % 4
+        got = D.rotate_bilinear_canvas(_t(srcs[si]), float(a), fl).cpu().numpy()
+        exp = out[:, ::-1] if fl & 1 else out
+        exp = exp[::-1] if fl & 2 else exp
+        assert got.shape == exp.shape and np.array_equal(got, exp), (si, a, fl)
+        crop = D.rotate_crop_bilinear(_t(srcs[si]), float(a)).cpu().numpy()
+        want = out if bb[0] < 0 else out[bb[1]:bb[3], bb[0]:bb[2]]
+        if want.shape[0] == 0 or want.shape[1] == 0:
+            want = out
+        assert np.array_equal(crop, want), (si, a)
+
+
+def test_rotate_bilinear_large_vs_oracle(D):
+    rng = np.random.default_rng(31)
+    img = rng.integers(0, 256, (300, 420, 4), np.uint8)
+    img[..., 3] = np.where(rng.random((300, 420)) < 0.2, 0, 255)
+    for a in (12.5, 45.0, 200.3):
+        got = D.rotate_crop_bilinear(_t(img), a).cpu().numpy()
+        assert np.array_equal(got, ops.rotate_and_crop(img, a, "bilinear")), a
+
+
+@pytest.mark.parametrize("i", range(6))
+def test_pipe_config3_geometry_matches_pillow(D, golden, i):
+    """The fused pipe (MFMA tap tiles at the ≈5× downscale of config 3) on a
+    1024² source, 896² crop, 1024² background, against the Pillow-only chain
+    (α = 255 everywhere through an HSV range that never matches)."""
+    from image_processor_pipeline_amd import fused
+    from tests.conftest import NEVER_RANGE, config3_item, sha256
+    g = golden("pipe_config3_pillow.npz")
+    src, bgs, (angle, sym, bgi, ratio, x, y) = config3_item(g, i)
+    cfg = fused.PipeConfig(hsv_ranges=[NEVER_RANGE])
+    plan = fused.plan_pipe((1024, 1024), 1, (1024, 1024), 2, cfg,
+                           params=[fused.ItemParams(angle, sym, bgi, ratio, x, y)])
+    assert plan.ov_dims[0] == tuple(int(v) for v in g["ov_wh"][i])[::-1]
+    runner = fused.PipeRunner(plan, DEV)
+    out = torch.empty((1, 1024, 1024, 3), dtype=torch.uint8, device=DEV)
+    runner.run(_t(src[None]), _t(bgs), out)
+    assert sha256(out[0].cpu().numpy()) == str(g["comp_sha"][i])

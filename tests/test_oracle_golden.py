@@ -70,3 +70,35 @@ def test_overlay_reference_composite_and_label(golden):
         got = ops.paste_rgba_onto_rgb(bg, rs, x, y)
         assert np.array_equal(got, comp)
         assert ops.yolo_label(0, x, y, nw, nh, bw, bh) == str(label)
+
+
+def test_bilinear_rotate_matches_pillow(golden):
+    """Opt-in BILINEAR mode: the oracle equals Pillow
+    rotate(..., resample=BILINEAR) canvases (RGB and RGBA) and their bbox."""
+    g = golden("rotate_bilinear_pillow.npz")
+    srcs = unpack(g["src_flat"], g["src_shapes"])
+    outs = unpack(g["out_flat"], g["out_shapes"])
+    for out, si, a, bb in zip(outs, g["src_index"], g["angles"], g["bboxes"]):
+        got = ops.rotate_expand_bilinear(ops.to_rgba(srcs[si]), float(a))
+        assert got.shape == out.shape and np.array_equal(got, out), (si, a)
+        gbb = ops.getbbox_alpha(got)
+        assert (gbb if gbb is not None else (-1, -1, -1, -1)) == tuple(bb)
+
+
+@pytest.mark.parametrize("i", [0, 3])
+def test_oracle_pipe_at_config3_geometry_matches_pillow(golden, i):
+    """BASELINE config-3 geometry (1024² source, 896² crop, ≈1266² rotated
+    cut-out, ≈5× LANCZOS downscale, paste on 1024²): the oracle's stages hash
+    to the Pillow chain's."""
+    from tests.conftest import config3_item, sha256
+    g = golden("pipe_config3_pillow.npz")
+    src, bgs, (angle, sym, bgi, ratio, x, y) = config3_item(g, i)
+    crop = ops.crop_from_border(src, (64, 64, 64, 64))
+    cut = ops.flip(ops.rotate_and_crop(ops.to_rgba(crop), angle), sym)
+    assert sha256(cut) == str(g["cut_sha"][i])
+    ov = ops.to_rgba(cut[..., :3])
+    nw, nh = ops.overlay_geometry(ov.shape[1], ov.shape[0], 1024, 1024, ratio)
+    assert (nw, nh) == tuple(int(v) for v in g["ov_wh"][i])
+    ovr = ops.resize_lanczos_rgba(ov, nw, nh)
+    assert sha256(ovr) == str(g["ov_sha"][i])
+    assert sha256(ops.paste_rgba_onto_rgb(bgs[bgi], ovr, x, y)) == str(g["comp_sha"][i])
