@@ -16,6 +16,11 @@ HOSTFLAGS := -O2 -std=c++17 -fPIC -Iinclude
 
 all: $(LIB)
 
+# Pillow's BILINEAR arithmetic is plain double mul/add (x86-64 baseline, no
+# FMA): this file must not contract a*b+c into fma, inlined HIP header
+# helpers included.
+$(OBJDIR)/ipp_bilinear.o: HIPFLAGS += -ffp-contract=off
+
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS) | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

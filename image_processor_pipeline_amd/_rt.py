@@ -40,7 +40,7 @@ def device() -> torch.device:
 def h2d(a: np.ndarray) -> torch.Tensor:
     if a.ndim == 2:
         a = a[..., None]
-    return torch.from_numpy(np.ascontiguousarray(a)).to(device())
+    return torch.from_numpy(np.require(a, requirements=["C", "W"])).to(device())
 
 
 def d2h(t: torch.Tensor) -> np.ndarray:

@@ -23,6 +23,10 @@ namespace {
 
 constexpr int BW = 64, BH = 4;
 
+// Built with -ffp-contract=off (Makefile): the pragma below covers this
+// file's expressions, the flag also covers the HIP header helpers inlined
+// here — a fused multiply-add changes the last bit that the truncation to
+// uint8 then exposes.
 #pragma clang fp contract(off)
 
 __device__ __forceinline__ uint32_t fetch_rgba_premul(const uint8_t* p, int cn) {
@@ -32,8 +36,8 @@ __device__ __forceinline__ uint32_t fetch_rgba_premul(const uint8_t* p, int cn) 
 }
 
 __device__ __forceinline__ double lerp_c(double a, double b, double d) {
-    // BILINEAR(v, a, b, d): v = a + (b - a) * d, two roundings, no FMA
-    return __dadd_rn(a, __dmul_rn(__dsub_rn(b, a), d));
+    // BILINEAR(v, a, b, d): v = a + (b - a) * d, separately rounded
+    return a + (b - a) * d;
 }
 
 __global__ void __launch_bounds__(256) k_rotate_bilinear(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -47,15 +51,15 @@ __global__ void __launch_bounds__(256) k_rotate_bilinear(const uint8_t* __restri
     if (x >= d.out_w || y >= d.out_h) return;
     const int cx = (d.flip & 1) ? d.out_w - 1 - x : x;   // canvas pixel this output shows
     const int cy = (d.flip & 2) ? d.out_h - 1 - y : y;
-    const double X = __dadd_rn((double)cx, 0.5), Y = __dadd_rn((double)cy, 0.5);
-    const double xin = __dadd_rn(__dadd_rn(__dmul_rn(d.m[0], X), __dmul_rn(d.m[1], Y)), d.m[2]);
-    const double yin = __dadd_rn(__dadd_rn(__dmul_rn(d.m[3], X), __dmul_rn(d.m[4], Y)), d.m[5]);
+    const double X = (double)cx + 0.5, Y = (double)cy + 0.5;
+    const double xin = (d.m[0] * X + d.m[1] * Y) + d.m[2];
+    const double yin = (d.m[3] * X + d.m[4] * Y) + d.m[5];
     uint32_t out = 0u;
     if (xin >= 0.0 && xin < (double)d.in_w && yin >= 0.0 && yin < (double)d.in_h) {
-        const double xs = __dsub_rn(xin, 0.5), ys = __dsub_rn(yin, 0.5);
+        const double xs = xin - 0.5, ys = yin - 0.5;
         const double xf = floor(xs), yf = floor(ys);
         const int xi = (int)xf, yi = (int)yf;
-        const double dx = __dsub_rn(xs, xf), dy = __dsub_rn(ys, yf);
+        const double dx = xs - xf, dy = ys - yf;
         const int x0 = min(max(xi, 0), d.in_w - 1), x1 = min(max(xi + 1, 0), d.in_w - 1);
         const int y0 = min(max(yi, 0), d.in_h - 1);
         const bool y1ok = yi + 1 >= 0 && yi + 1 < d.in_h;
