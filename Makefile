@@ -5,7 +5,8 @@ ARCH ?= gfx950
 PKG := image_processor_pipeline_amd
 CSRC := $(PKG)/csrc
 SRCS := $(CSRC)/ipp_gather.hip $(CSRC)/ipp_hsv.hip $(CSRC)/ipp_resample.hip $(CSRC)/ipp_pipe.hip \
-        $(CSRC)/ipp_ccl.hip $(CSRC)/ipp_util.hip $(CSRC)/ipp_bilinear.hip
+        $(CSRC)/ipp_ccl.hip $(CSRC)/ipp_util.hip $(CSRC)/ipp_bilinear.hip \
+        $(CSRC)/ipp_enhance.hip
 HOST_SRCS := $(CSRC)/ipp_host.cpp
 HDRS := include/ipp.h $(wildcard $(CSRC)/*.h)
 OBJDIR := build/obj
@@ -16,10 +17,10 @@ HOSTFLAGS := -O2 -std=c++17 -fPIC -Iinclude
 
 all: $(LIB)
 
-# Pillow's BILINEAR arithmetic is plain double mul/add (x86-64 baseline, no
-# FMA): this file must not contract a*b+c into fma, inlined HIP header
-# helpers included.
-$(OBJDIR)/ipp_bilinear.o: HIPFLAGS += -ffp-contract=off
+# Pillow's BILINEAR (double) and Blend (float) arithmetic is plain mul/add
+# (x86-64 baseline, no FMA): these files must not contract a*b+c into fma,
+# inlined HIP header helpers included.
+$(OBJDIR)/ipp_bilinear.o $(OBJDIR)/ipp_enhance.o: HIPFLAGS += -ffp-contract=off
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS) | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

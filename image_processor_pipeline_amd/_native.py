@@ -52,6 +52,14 @@ AFFINE_DESC = np.dtype([
     ("out_w", _I4), ("out_h", _I4), ("dst_pitch", _I4), ("flip", _I4), ("m", np.float64, (6,)),
 ], align=True)
 
+IPP_ENH_BLUR = 1
+IPP_ENH_LUT = 2
+ENHANCE_DESC = np.dtype([
+    ("src_off", _I8), ("dst_off", _I8), ("w", _I4), ("h", _I4), ("src_pitch", _I4), ("dst_pitch", _I4),
+    ("f_brightness", np.float32), ("f_contrast", np.float32), ("f_color", np.float32), ("flags", _I4),
+    ("box_r", _I4), ("box_ww", np.uint32), ("box_fw", np.uint32), ("pad_", _I4), ("lut_off", _I8),
+], align=True)
+
 COPY_DESC = np.dtype([
     ("src_off", _I8), ("dst_off", _I8), ("src_pitch", _I4), ("dst_pitch", _I4),
     ("x0", _I4), ("y0", _I4), ("w", _I4), ("h", _I4), ("cn", _I4), ("flip", _I4),
@@ -114,6 +122,9 @@ SIGNATURES = {
     "ipp_plan_mfma_nk_bound": (_I, [_I, _I, _I]),
     "ipp_plan_pipe_axes": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _I]),
     "ipp_stream_copy": (_I, [_P, _P, _L, _P]),
+    "ipp_enhance_lsum": (_I, [_P, _P, _I, _L, _P, _P]),
+    "ipp_enhance_color": (_I, [_P, _P, _P, _I, _L, _P, _P, _P]),
+    "ipp_box_pass": (_I, [_P, _P, _P, _I, _L, _P, _I, _P, _I, _P]),
     "ipp_pipe_status": (_I, [_P, _P]),
     "ipp_version": (ctypes.c_char_p, []),
 }

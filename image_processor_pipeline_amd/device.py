@@ -325,3 +325,91 @@ def paste_blend(bg: torch.Tensor, ov: torch.Tensor, x: int, y: int) -> torch.Ten
                                      _stream(bg.device)), "ipp_paste_blend")
     _keep(dd)
     return out
+
+
+# ---------------------------------------------------------------------------
+# tranfo.enhance_image (tranfo.py:37-53): brightness / contrast / color
+# blends, GaussianBlur box passes, per-channel LUTs
+# ---------------------------------------------------------------------------
+
+@dataclass
+class EnhanceParams:
+    brightness: float
+    contrast: float
+    color: float
+    blur_radius: Optional[float] = None        # GaussianBlur radius, None = no blur
+    luts: Optional[np.ndarray] = None           # uint8 (3, 256) r/g/b tables, None = no point()
+
+
+def enhance_rgb(imgs: Sequence[torch.Tensor], params: Sequence[EnhanceParams]) -> List[torch.Tensor]:
+    """Batched tranfo.enhance_image pixel chain on (H, W, 3) RGB tensors:
+    one ipp_enhance_lsum + one ipp_enhance_color launch for the whole batch,
+    plus 6 ipp_box_pass launches when any image is blurred."""
+    n = len(imgs)
+    if n == 0:
+        return []
+    dev = imgs[0].device
+    lib = N.load()
+    d = np.zeros(n, N.ENHANCE_DESC)
+    luts = np.zeros((n, 3, 256), np.uint8)
+    src_parts, off = [], 0
+    max_px = 1
+    any_blur = any_lut = False
+    for i, (im, p) in enumerate(zip(imgs, params)):
+        _require_cuda(im, "enhance_rgb")
+        h, w, cn = im.shape
+        if cn != 3:
+            raise ValueError("enhance_rgb expects RGB images (tranfo.py:37 converts to RGB)")
+        d[i]["src_off"] = d[i]["dst_off"] = off
+        d[i]["w"], d[i]["h"], d[i]["src_pitch"], d[i]["dst_pitch"] = w, h, 3 * w, 3 * w
+        d[i]["f_brightness"], d[i]["f_contrast"], d[i]["f_color"] = p.brightness, p.contrast, p.color
+        flags = 0
+        if p.blur_radius is not None:
+            r, ww, fw, fr = G.gaussian_box(p.blur_radius)
+            if fr != 0.0:
+                flags |= N.IPP_ENH_BLUR
+                d[i]["box_r"], d[i]["box_ww"], d[i]["box_fw"] = r, ww, fw
+                any_blur = True
+        if p.luts is not None:
+            flags |= N.IPP_ENH_LUT
+            luts[i] = p.luts
+            any_lut = True
+        d[i]["flags"] = flags
+        d[i]["lut_off"] = i * 768
+        src_parts.append(im.contiguous().reshape(-1))
+        off += h * w * 3
+        max_px = max(max_px, h * w)
+    src = torch.cat(src_parts) if n > 1 else src_parts[0]
+    out = torch.empty_like(src)
+    dd = _to_dev(d, dev)
+    ld = _to_dev(luts, dev) if any_lut else None
+    sums = torch.empty(n, dtype=torch.int64, device=dev)
+    st = _stream(dev)
+    N.check(lib.ipp_enhance_lsum(src.data_ptr(), dd.data_ptr(), n, max_px, sums.data_ptr(), st), "ipp_enhance_lsum")
+    N.check(lib.ipp_enhance_color(src.data_ptr(), out.data_ptr(), dd.data_ptr(), n, max_px, sums.data_ptr(),
+                                  ld.data_ptr() if ld is not None else None, st), "ipp_enhance_color")
+    keep = [dd, sums] + ([ld] if ld is not None else [])
+    if any_blur:
+        # blurred images only: 3 row passes then 3 column passes, ping-pong
+        bi = [i for i in range(n) if d[i]["flags"] & N.IPP_ENH_BLUR]
+        bd = d[bi].copy()
+        offs = np.array([int(d[i]["src_off"]) for i in bi], np.int64)
+        bdd, od = _to_dev(bd, dev), _to_dev(offs, dev)
+        tmp = torch.empty_like(src)
+        a, b = out, tmp
+        bmax = max(int(bd[k]["w"]) * int(bd[k]["h"]) for k in range(len(bi)))
+        for k in range(6):
+            last = k == 5
+            N.check(lib.ipp_box_pass(a.data_ptr(), (out if last else b).data_ptr(), bdd.data_ptr(), len(bi), bmax,
+                                     od.data_ptr(), 0 if k < 3 else 1,
+                                     ld.data_ptr() if (last and ld is not None) else None, 0, st), "ipp_box_pass")
+            if not last:
+                a, b = b, a
+        keep += [bdd, od, tmp]
+    _keep(*keep)
+    res = []
+    for i, im in enumerate(imgs):
+        h, w, _ = im.shape
+        o = int(d[i]["src_off"])
+        res.append(out[o:o + h * w * 3].view(h, w, 3))
+    return res

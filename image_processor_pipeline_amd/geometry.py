@@ -235,3 +235,23 @@ def identity_taps(n: int) -> Tuple[int, np.ndarray]:
     buf[1:2 * n:2] = 1
     buf[2 * n:] = 1 << 22
     return 1, buf
+
+
+def gaussian_box(radius: float, passes: int = 3) -> Tuple[int, int, int, float]:
+    """ImageFilter.GaussianBlur(radius) (tranfo.py:44) → the box pass of
+    libImaging BoxBlur.c: ``_gaussian_blur_radius`` in float32 (sqrt and
+    floor in double), then ImagingHorizontalBoxBlur's integer radius and
+    8.24 weights ww = (uint32)(2^24 / (2·r_f + 1)), fw = (2^24 - (2r+1)·ww) / 2.
+    Returns (r, ww, fw, r_f); r_f == 0 means no blur."""
+    f32 = np.float32
+    r = f32(radius)
+    sigma2 = f32(r * r / f32(passes))
+    L = f32(math.sqrt(12.0 * float(sigma2) + 1.0))
+    l = f32(math.floor((float(L) - 1.0) / 2.0))
+    a = f32((f32(2) * l + f32(1)) * (l * (l + f32(1)) - f32(3) * sigma2))
+    a = f32(a / (f32(6) * (sigma2 - (l + f32(1)) * (l + f32(1)))))
+    fr = f32(l + a)
+    ir = int(fr)
+    ww = int(f32(1 << 24) / (fr * f32(2) + f32(1)))
+    fw = ((1 << 24) - (2 * ir + 1) * ww) // 2
+    return ir, ww, fw, float(fr)

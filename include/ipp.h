@@ -349,6 +349,41 @@ int ipp_plan_opaque_bbox(int32_t in_w, int32_t in_h, const int32_t a[6],
                          int32_t nw, int32_t nh, int32_t bbox[4]);
 
 /* ------------------------------------------------------------------------ */
+/* tranfo.enhance_image (transforms/tranfo.py:37-53) on RGB images:           */
+/* ImageEnhance Brightness/Contrast/Color (:38-40, Image.blend, Blend.c),     */
+/* GaussianBlur (:42-44, BoxBlur.c) and the r/g/b point() LUTs (:46-51).      */
+/* ------------------------------------------------------------------------ */
+#define IPP_ENH_BLUR 1   /* a GaussianBlur follows (box passes, ipp_box_pass) */
+#define IPP_ENH_LUT 2    /* apply the image's 3×256 LUT (after the blur)      */
+
+typedef struct ipp_enhance_desc {
+    int64_t src_off, dst_off;          /* RGB images, explicit pitches      */
+    int32_t w, h, src_pitch, dst_pitch;
+    float f_brightness, f_contrast, f_color;  /* float32(factor), Blend.c   */
+    int32_t flags;                     /* IPP_ENH_*                          */
+    int32_t box_r;                     /* box radius (int part), BoxBlur.c   */
+    uint32_t box_ww, box_fw;           /* 8.24 weights of the box pass       */
+    int32_t pad_;
+    int64_t lut_off;                   /* byte offset of 3×256 LUT bytes     */
+} ipp_enhance_desc;
+
+/* Σ L of the brightened image per image into sums[n] (zeroed first). */
+int ipp_enhance_lsum(const uint8_t* src, const ipp_enhance_desc* descs, int32_t n_images,
+                     int64_t max_pixels, uint64_t* sums, void* stream);
+/* brightness → contrast (mean = int(Σ/N + 0.5)) → color [→ LUT when the
+ * image has IPP_ENH_LUT and no IPP_ENH_BLUR]; writes dst (dst_off/pitch). */
+int ipp_enhance_color(const uint8_t* src, uint8_t* dst, const ipp_enhance_desc* descs,
+                      int32_t n_images, int64_t max_pixels, const uint64_t* sums,
+                      const uint8_t* luts, void* stream);
+/* One BoxBlur.c pass along x (axis 0) or y (axis 1) of packed RGB planes at
+ * byte offsets offs[i] (pitch 3w) in src → dst at the same offsets, or at the
+ * descriptor's dst_off/dst_pitch when final_dst; luts != NULL applies the
+ * LUTs (last pass).  A GaussianBlur is 3 x passes then 3 y passes. */
+int ipp_box_pass(const uint8_t* src, uint8_t* dst, const ipp_enhance_desc* descs, int32_t n_images,
+                 int64_t max_pixels, const int64_t* offs, int32_t axis, const uint8_t* luts,
+                 int32_t final_dst, void* stream);
+
+/* ------------------------------------------------------------------------ */
 /* Measurement helper (the copy-kernel ceiling of the box).     */
 /* ------------------------------------------------------------------------ */
 /* dst[0, nbytes) = src[0, nbytes) with 16-B non-temporal loads/stores; both

@@ -504,3 +504,119 @@ def keep_largest_component(img_bgra: np.ndarray) -> np.ndarray:
         raise ValueError("no non-transparent pixel (cv2.boundingRect(None))")
     cols = np.flatnonzero((a != 0).any(axis=0))
     return out[rows[0]:rows[-1] + 1, cols[0]:cols[-1] + 1].copy()
+
+
+# ---------------------------------------------------------------------------
+# tranfo.enhance_image (transforms/tranfo.py:37-53): ImageEnhance Brightness /
+# Contrast / Color, ImageFilter.GaussianBlur, per-channel point() LUTs.
+# Library: PIL/ImageEnhance.py (degenerate images + Image.blend), libImaging
+# Blend.c (float32 blend, truncation; clipped extrapolation), Convert.c
+# rgb2l (L = (19595 R + 38470 G + 7471 B + 0x8000) >> 16), ImageStat mean,
+# BoxBlur.c (Gaussian = 3 box passes per axis, 8.24 fixed point).
+# ---------------------------------------------------------------------------
+
+def blend(im1: np.ndarray, im2: np.ndarray, factor: float) -> np.ndarray:
+    """Image.blend(im1, im2, factor): Blend.c with alpha = float32(factor)."""
+    a = np.float32(factor)
+    if a == np.float32(0.0):
+        return im1.copy()
+    if a == np.float32(1.0):
+        return im2.copy()
+    i1 = im1.astype(np.float32)
+    d = (im2.astype(np.int32) - im1.astype(np.int32)).astype(np.float32)
+    t = i1 + a * d                      # two float32 roundings (no FMA)
+    if np.float32(0.0) <= a <= np.float32(1.0):
+        return t.astype(np.uint8)       # (UINT8) truncation
+    out = np.where(t <= 0.0, 0, np.where(t >= 255.0, 255, t))
+    return out.astype(np.uint8)
+
+
+def rgb_to_l(img: np.ndarray) -> np.ndarray:
+    """Convert.c rgb2l."""
+    r, g, b = (img[..., k].astype(np.int64) for k in range(3))
+    return ((r * 19595 + g * 38470 + b * 7471 + 0x8000) >> 16).astype(np.uint8)
+
+
+def enhance_brightness(img: np.ndarray, f: float) -> np.ndarray:
+    return blend(np.zeros_like(img), img, f)
+
+
+def enhance_contrast(img: np.ndarray, f: float) -> np.ndarray:
+    lum = rgb_to_l(img)
+    s = float(np.sum(lum, dtype=np.int64))           # ImageStat sum (exact in double)
+    mean = int(s / lum.size + 0.5)
+    return blend(np.full_like(img, mean), img, f)
+
+
+def enhance_color(img: np.ndarray, f: float) -> np.ndarray:
+    lum = rgb_to_l(img)
+    return blend(np.repeat(lum[..., None], 3, axis=2), img, f)
+
+
+def gaussian_box_radius(radius: float, passes: int = 3) -> float:
+    """BoxBlur.c _gaussian_blur_radius in float32 (sqrt/floor in double)."""
+    r = np.float32(radius)
+    sigma2 = np.float32(r * r / np.float32(passes))
+    L = np.float32(math.sqrt(12.0 * float(sigma2) + 1.0))
+    l = np.float32(math.floor((float(L) - 1.0) / 2.0))
+    a = np.float32((np.float32(2) * l + np.float32(1)) * (l * (l + np.float32(1)) - np.float32(3) * sigma2))
+    a = np.float32(a / (np.float32(6) * (sigma2 - (l + np.float32(1)) * (l + np.float32(1)))))
+    return float(np.float32(l + a))
+
+
+def box_blur_rows(img: np.ndarray, fradius: float) -> np.ndarray:
+    """BoxBlur.c ImagingHorizontalBoxBlur on every row (uint32 fixed point):
+    out[x] = (acc(x)·ww + (in[x-r-1] + in[x+r+1])·fw + 2^23) >> 24 with
+    acc(x) = Σ in[clamp(i)], i ∈ [x-r, x+r], indices clamped to the row."""
+    fr = np.float32(fradius)
+    r = int(fr)
+    ww = int(np.float32(1 << 24) / (fr * np.float32(2) + np.float32(1)))
+    fw = ((1 << 24) - (2 * r + 1) * ww) // 2
+    h, w = img.shape[:2]
+    src = img.astype(np.int64)
+    idx = np.arange(w)
+    acc = np.zeros_like(src)
+    for i in range(-r, r + 1):
+        acc += src[:, np.clip(idx + i, 0, w - 1)]
+    far = src[:, np.clip(idx - r - 1, 0, w - 1)] + src[:, np.clip(idx + r + 1, 0, w - 1)]
+    bulk = (acc * ww + far * fw) & 0xFFFFFFFF
+    return (((bulk + (1 << 23)) & 0xFFFFFFFF) >> 24).astype(np.uint8)
+
+
+def gaussian_blur(img: np.ndarray, radius: float, passes: int = 3) -> np.ndarray:
+    """ImageFilter.GaussianBlur(radius) (tranfo.py:44): BoxBlur.c
+    ImagingGaussianBlur → ImagingBoxBlur with the same box radius on both axes."""
+    br = gaussian_box_radius(radius, passes)
+    out = img.copy()
+    if br == 0.0:
+        return out
+    for _ in range(passes):
+        out = box_blur_rows(out, br)
+    t = np.ascontiguousarray(out.transpose(1, 0, 2))
+    for _ in range(passes):
+        t = box_blur_rows(t, br)
+    return np.ascontiguousarray(t.transpose(1, 0, 2))
+
+
+def point_luts(rng_uniform, lo: float = 0.75, hi: float = 1.25) -> np.ndarray:
+    """tranfo.py:48-50: for r, g, b in turn, Image.point calls the lambda for
+    p = 0..255 (one uniform draw each) and rounds: round(max(0, min(255, p·u)))."""
+    luts = np.zeros((3, 256), np.uint8)
+    for c in range(3):
+        for p in range(256):
+            luts[c, p] = round(max(0, min(255, p * rng_uniform(lo, hi))))
+    return luts
+
+
+def enhance_image(img_rgb: np.ndarray, apply_blur: bool, apply_rgb: bool, rnd) -> np.ndarray:
+    """tranfo.enhance_image pixel chain with the draws taken from `rnd`
+    (a random.Random or the random module) in the reference order."""
+    out = enhance_brightness(img_rgb, rnd.uniform(0.7, 1.3))
+    out = enhance_contrast(out, rnd.uniform(0.7, 1.3))
+    out = enhance_color(out, rnd.uniform(0.7, 1.3))
+    if apply_blur:
+        out = gaussian_blur(out, rnd.uniform(0.5, 3))
+    if apply_rgb:
+        luts = point_luts(rnd.uniform)
+        out = np.stack([luts[c][out[..., c]] for c in range(3)], axis=-1)
+    return out

@@ -41,6 +41,7 @@ STRUCTS = {
     "ipp_pipe_desc": N.PIPE_DESC,
     "ipp_ccl_work": N.CCL_WORK,
     "ipp_affine_desc": N.AFFINE_DESC,
+    "ipp_enhance_desc": N.ENHANCE_DESC,
 }
 
 

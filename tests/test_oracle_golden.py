@@ -102,3 +102,16 @@ def test_oracle_pipe_at_config3_geometry_matches_pillow(golden, i):
     ovr = ops.resize_lanczos_rgba(ov, nw, nh)
     assert sha256(ovr) == str(g["ov_sha"][i])
     assert sha256(ops.paste_rgba_onto_rgb(bgs[bgi], ovr, x, y)) == str(g["comp_sha"][i])
+
+
+def test_enhance_image_reference_outputs(golden):
+    """tranfo.enhance_image: the oracle (Blend.c / rgb2l / ImageStat /
+    BoxBlur.c / point() restated) with the draws taken in the reference order
+    reproduces the reference's own outputs (tests/golden/tranfo_ref.npz)."""
+    g = golden("tranfo_ref.npz")
+    srcs = unpack(g["src_flat"], g["src_shapes"])
+    outs = unpack(g["out_flat"], g["out_shapes"])
+    for s, o, (blur, rgb), seed in zip(srcs, outs, g["flags"], g["seeds"]):
+        rnd = random.Random(int(seed))
+        got = ops.enhance_image(s[..., :3].copy(), bool(blur), bool(rgb), rnd)
+        assert np.array_equal(got, o), (s.shape, blur, rgb)

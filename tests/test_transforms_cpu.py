@@ -133,3 +133,26 @@ def test_device_path_fails_loudly_without_gpu(tmp_path):
     Image.fromarray(np.zeros((10, 10, 3), np.uint8)).save(q)
     with pytest.raises(N.NativeUnavailable):
         recadrages.crop_from_border(q, [tmp_path], crop_margins=(1, 1, 1, 1))
+
+
+def test_change_label_class_reference_kat(tmp_path, capsys):
+    """labels.py's own known-answer check (:67-128) with its intended call
+    (cls_mapping=, output dir created); as written it passes
+    class_id_mapping= (ignored → identity {0: 0}) into a missing dir (→ None)."""
+    from image_processor_pipeline_amd.transforms import labels
+    src = tmp_path / "in" / "test_label.txt"
+    src.parent.mkdir()
+    src.write_text("0 0.5 0.5 0.1 0.1\n1 0.2 0.2 0.1 0.1\n0 0.8 0.8 0.1 0.1\n2 0.3 0.3 0.1 0.1\n", encoding="utf-8")
+    out_dir = tmp_path / "out"
+    assert labels.change_label_class(input_path=src, output_dirs=[out_dir], class_id_mapping={0: 99, 1: 77}) is None
+    assert "Problème" in capsys.readouterr().out
+    out_dir.mkdir()
+    res = labels.change_label_class(input_path=src, output_dirs=[out_dir], cls_mapping={0: 99, 1: 77})
+    assert res == out_dir / "test_label.txt"
+    assert res.read_text(encoding="utf-8") == ("99 0.5 0.5 0.1 0.1\n77 0.2 0.2 0.1 0.1\n"
+                                               "99 0.8 0.8 0.1 0.1\n2 0.3 0.3 0.1 0.1\n")
+    res = labels.change_label_class(src, [out_dir], class_id_mapping={0: 99})
+    assert res.read_text(encoding="utf-8") == src.read_text(encoding="utf-8")
+    bad = tmp_path / "in" / "bad.txt"
+    bad.write_text("x 1 2 3 4\n")
+    assert labels.change_label_class(bad, [out_dir]) is None and not (out_dir / "bad.txt").exists()
