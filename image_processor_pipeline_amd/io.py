@@ -14,7 +14,7 @@ from pathlib import Path
 from typing import Optional
 
 import numpy as np
-from PIL import Image
+from PIL import Image, ImageOps
 
 IMREAD_UNCHANGED = -1
 IMREAD_GRAYSCALE = 0
@@ -27,21 +27,37 @@ VID_FORMATS = {"asf", "avi", "gif", "m4v", "mkv", "mov", "mp4", "mpeg", "mpg", "
 
 
 def imread(path, flags: int = IMREAD_COLOR) -> Optional[np.ndarray]:
-    """cv2.imread: None when the file is missing or not decodable."""
+    """cv2.imread: None when the file is missing or not decodable.
+
+    Like OpenCV, IMREAD_COLOR and IMREAD_GRAYSCALE apply the EXIF orientation
+    tag (camera JPEGs come out upright, so crop_square's YOLO boxes land on
+    the right pixels) and IMREAD_UNCHANGED does not.  IMREAD_UNCHANGED keeps
+    16-bit single-channel images as uint16 (and 32-bit float ones as
+    float32), as cv2 does; other deep modes are refused (None)."""
     try:
         with Image.open(str(path)) as im:
             im.load()
             mode = im.mode
-            if flags == IMREAD_GRAYSCALE:
-                return np.asarray(im.convert("L")).copy()
             if flags == IMREAD_UNCHANGED:
                 if mode in ("RGBA", "LA", "PA") or (mode == "P" and "transparency" in im.info):
                     arr = np.asarray(im.convert("RGBA"))
                     return arr[..., [2, 1, 0, 3]].copy()
-                if mode in ("L", "I;16", "I", "F", "1"):
+                if mode.startswith("I;16"):
+                    return np.asarray(im).astype(np.uint16)
+                if mode == "I":
+                    arr = np.asarray(im)
+                    if arr.size and (arr.min() < 0 or arr.max() > 65535):
+                        return None
+                    return arr.astype(np.uint16)
+                if mode == "F":
+                    return np.asarray(im).astype(np.float32)
+                if mode in ("L", "1"):
                     return np.asarray(im.convert("L")).copy()
                 arr = np.asarray(im.convert("RGB"))
                 return arr[..., ::-1].copy()
+            im = ImageOps.exif_transpose(im)
+            if flags == IMREAD_GRAYSCALE:
+                return np.asarray(im.convert("L")).copy()
             arr = np.asarray(im.convert("RGB"))
             return arr[..., ::-1].copy()
     except (FileNotFoundError, OSError, ValueError):
@@ -53,7 +69,11 @@ def imwrite(path, img: np.ndarray) -> bool:
     path = str(path)
     ext = Path(path).suffix.lower()
     try:
-        if img.ndim == 2:
+        if img.dtype == np.uint16 and img.ndim == 2:
+            im = Image.fromarray(img)            # 16-bit grayscale PNG/TIFF, as cv2 writes it
+        elif img.dtype != np.uint8:
+            return False
+        elif img.ndim == 2:
             im = Image.fromarray(img, "L")
         elif img.shape[2] == 4:
             im = Image.fromarray(np.ascontiguousarray(img[..., [2, 1, 0, 3]]), "RGBA")

@@ -11,6 +11,8 @@ from pathlib import Path
 from typing import Any, List, Optional
 from warnings import warn
 
+import numpy as np
+
 from ._common import device_transform
 from .. import _rt
 from .. import device as D
@@ -56,10 +58,20 @@ def generate_symmetries(
         filter_.append("o")
 
     gray = image.ndim == 2
+    dtype = image.dtype
+    if dtype != np.uint8:
+        # deep images (16-bit PNG via IMREAD_UNCHANGED): flip whole pixels as
+        # byte groups (cv2.flip is dtype-agnostic)
+        if image.itemsize * (1 if gray else image.shape[2]) > 4:
+            raise ValueError(f"[{input_path.name} - Symétrie] format de pixel non pris en charge ({dtype}).")
+        h, w = image.shape[:2]
+        image = np.ascontiguousarray(image).view(np.uint8).reshape(h, w, -1)
     img_dev = _rt.h2d(image)
     saved_files: List[Path] = []
     for sym in filter_:
         out = _rt.d2h(D.flip(img_dev, sym))
+        if dtype != np.uint8:
+            out = np.ascontiguousarray(out).view(dtype).reshape(out.shape[0], out.shape[1], -1)
         if gray:
             out = out[..., 0]
         output_filename = input_path.with_stem(f"{input_path.stem}_{sym}")

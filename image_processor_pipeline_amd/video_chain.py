@@ -138,3 +138,22 @@ def synthetic_frames(n: int, h: int, w: int, seed: int, device, start: int = 0) 
         k = int(speck.sum())
         frame[speck] = torch.randint(0, 256, (k, 3), generator=g, device=dev, dtype=torch.uint8)
     return out
+
+
+def keep_largest_from_video(video_path, batch: int = 32, device="cuda", ranges=None, zones=None,
+                            use_gimp_scale: bool = False) -> List[Optional[np.ndarray]]:
+    """video.frame_extraction → filtres_liste → pixels_isolés for one video,
+    frames decoded on the host (transforms.video.open_video) and run through
+    the fused device chain in batches of `batch` frames, without the JPEG
+    files between the steps.  Returns one BGRA crop (or None) per frame."""
+    from .transforms.video import iter_frame_batches
+    out: List[Optional[np.ndarray]] = []
+    chain = None
+    for fr in iter_frame_batches(video_path, batch):
+        n, h, w, _ = fr.shape
+        if chain is None or (chain.n, chain.h, chain.w) != (n, h, w):
+            chain = VideoChain(n, h, w, device, ranges, zones, use_gimp_scale)
+        t = torch.from_numpy(fr).to(chain.device)
+        chain.run(t)
+        out.extend(chain.results())
+    return out

@@ -156,3 +156,61 @@ def test_change_label_class_reference_kat(tmp_path, capsys):
     bad = tmp_path / "in" / "bad.txt"
     bad.write_text("x 1 2 3 4\n")
     assert labels.change_label_class(bad, [out_dir]) is None and not (out_dir / "bad.txt").exists()
+
+
+def _gif(path, frames):
+    from PIL import Image
+    ims = [Image.fromarray(f, "RGB") for f in frames]
+    ims[0].save(path, save_all=True, append_images=ims[1:], duration=40, loop=0)
+
+
+def test_frame_extraction_reference_layout(tmp_path):
+    """video.py:6-47: <out>/<stem>/0-raw/{basename}-frame_{n:04d}.jpg from n=1,
+    the reference's checks in the reference's order (GIF decoded by Pillow:
+    OpenCV/FFmpeg are absent here)."""
+    from image_processor_pipeline_amd import io as ipp_io
+    from image_processor_pipeline_amd.transforms import video
+    rng = np.random.default_rng(3)
+    frames = [np.zeros((24, 32, 3), np.uint8) + rng.integers(0, 2, 3, np.uint8) * 200 for _ in range(3)]
+    for k, f in enumerate(frames):
+        f[4 + k:12 + k, 5:20] = (250, 40, 10)
+    _gif(tmp_path / "clip.gif", frames)
+    with pytest.raises(ValueError):
+        video.frame_extraction(tmp_path / "clip.gif", [tmp_path / "out"], "")
+    d = video.frame_extraction(tmp_path / "clip.gif", [tmp_path / "out"], "cls")
+    assert d == tmp_path / "out" / "clip" / "0-raw"
+    assert sorted(p.name for p in d.iterdir()) == [f"cls-frame_{n:04d}.jpg" for n in (1, 2, 3)]
+    dec = list(video.open_video(tmp_path / "clip.gif"))
+    assert len(dec) == 3 and dec[0].shape == (24, 32, 3)
+    for n, f in enumerate(dec, start=1):       # the JPEG written is the BGR frame, encoded at quality 95
+        q = tmp_path / f"q{n}.jpg"
+        ipp_io.imwrite(q, f)
+        assert np.array_equal(ipp_io.imread(d / f"cls-frame_{n:04d}.jpg"), ipp_io.imread(q))
+    batches = list(video.iter_frame_batches(tmp_path / "clip.gif", 2))
+    assert [b.shape[0] for b in batches] == [2, 1] and np.array_equal(np.concatenate(batches), np.stack(dec))
+    (tmp_path / "bad.mp4").write_bytes(b"not a video")
+    with pytest.raises(RuntimeError):
+        video.frame_extraction(tmp_path / "bad.mp4", [tmp_path / "out"], "cls")
+    from PIL import Image
+    Image.fromarray(frames[0]).save(tmp_path / "still.png")
+    with pytest.raises(ValueError):     # opens, but .png is not a VID_FORMATS suffix
+        video.frame_extraction(tmp_path / "still.png", [tmp_path / "out"], "cls")
+
+
+def test_io_exif_orientation_and_16bit(tmp_path):
+    """cv2.imread semantics: IMREAD_COLOR applies the EXIF
+    orientation, IMREAD_UNCHANGED does not; 16-bit PNGs stay uint16."""
+    from PIL import Image
+    from image_processor_pipeline_amd import io as ipp_io
+    rgb = np.random.default_rng(0).integers(0, 256, (20, 30, 3), np.uint8)
+    im = Image.fromarray(rgb)
+    ex = im.getexif()
+    ex[0x0112] = 6                       # rotate 90° CW on display
+    im.save(tmp_path / "e.jpg", exif=ex, quality=100)
+    assert ipp_io.imread(tmp_path / "e.jpg").shape == (30, 20, 3)
+    assert ipp_io.imread(tmp_path / "e.jpg", ipp_io.IMREAD_GRAYSCALE).shape == (30, 20)
+    assert ipp_io.imread(tmp_path / "e.jpg", ipp_io.IMREAD_UNCHANGED).shape == (20, 30, 3)
+    a16 = (np.arange(12 * 7, dtype=np.uint16).reshape(12, 7) * 700)
+    assert ipp_io.imwrite(tmp_path / "d.png", a16)
+    back = ipp_io.imread(tmp_path / "d.png", ipp_io.IMREAD_UNCHANGED)
+    assert back.dtype == np.uint16 and np.array_equal(back, a16)
