@@ -19,8 +19,9 @@ from typing import Any, List, Optional, Tuple
 import numpy as np
 from PIL import Image, UnidentifiedImageError
 
-from ._common import device_transform
+from ._common import batch_run, device_transform
 from .. import _rt
+from .. import batch_ops as BO
 from .. import device as D
 from .. import geometry as G
 from ..labels_math import xyxy2xywhn
@@ -108,3 +109,100 @@ def paste_overlay_onto_background(
             except OSError:
                 print(f"Avertissement: Impossible de nettoyer le fichier partiellement créé {p}")
         return None
+
+
+def _overlays_batch(arg_tuples, output_dirs: List[Path], threads: int = 1, yolo_class_id: int = 0,
+                    scale_min: float = 0.15, scale_max: float = 0.30, **options: Any) -> List:
+    """Batched paste_overlay_onto_background ('modulo' pairs): decode on host
+    threads, the per-item draws (uniform ratio, then two randint) in pair
+    order, ONE batched LANCZOS H + V + paste launch set for the chunk
+    (batch_ops.overlays), encode + label on host threads.  Messages and
+    None results as in the per-file path."""
+    image_target_dir, label_target_dir = utils._validate_dirs(output_dirs, nb_dirs=2)
+
+    def load(args):
+        overlay_path, background_path = args[0], args[1]
+        names = f"[{overlay_path.name} + {background_path.name}]"
+        try:
+            overlay = Image.open(overlay_path)
+            if overlay.mode != "RGBA":
+                overlay = overlay.convert("RGBA")
+            background = Image.open(background_path).convert("RGB")
+            return np.asarray(overlay), np.asarray(background)
+        except FileNotFoundError as fnf:
+            print(f"Erreur {names}: Fichier non trouvé: {fnf}")
+        except UnidentifiedImageError as uie:
+            print(f"Erreur {names}: Impossible d'ouvrir l'image {uie}")
+        except TypeError as te:
+            print(f"Erreur {names}: Type d'image invalide : {te}")
+        except Exception as e:
+            print(f"Erreur {names}: Échec lecture fichiers: {e}")
+        return None
+
+    def compute(items, args):
+        plans, ovs, bgs, sizes, pos = [], [], [], [], []
+        for item, a in zip(items, args):
+            if item is None:
+                plans.append(None)
+                continue
+            ov, bg = item
+            names = f"[{a[0].name} + {a[1].name}]"
+            try:
+                bh, bw = bg.shape[:2]
+                target_ratio = random.uniform(scale_min, scale_max)
+                if ov.shape[0] == 0:
+                    raise ValueError(f"dimensions de l'overlay {a[0].name} invalides ({ov.shape[1]}x{ov.shape[0]}).")
+                new_w, new_h = G.overlay_size(ov.shape[1], ov.shape[0], bw, bh, target_ratio)
+                if new_w <= 0 or new_h <= 0:
+                    raise ValueError("height and width must be > 0")
+                pos_x = random.randint(0, bw - new_w)
+                pos_y = random.randint(0, bh - new_h)
+            except ValueError as ve:
+                print(f"Erreur de valeur {names}: {ve}")
+                plans.append(None)
+                continue
+            except Exception as e:
+                print(f"Erreur {names}: Échec pendant le processus de superposition: {e}")
+                plans.append(None)
+                continue
+            plans.append((len(ovs), (new_w, new_h), (pos_x, pos_y), (bw, bh)))
+            ovs.append(ov)
+            bgs.append(bg)
+            sizes.append((new_w, new_h))
+            pos.append((pos_x, pos_y))
+        comps = BO.overlays(ovs, bgs, sizes, pos) if ovs else []
+        return [None if p is None else (comps[p[0]], p) for p in plans]
+
+    def save(args, _item, res):
+        if res is None:
+            return None
+        comp, (_, (new_w, new_h), (pos_x, pos_y), (bw, bh)) = res
+        overlay_path, background_path = args[0], args[1]
+        names = f"[{overlay_path.name} + {background_path.name}]"
+        bbox = np.array([pos_x, pos_y, pos_x + new_w, pos_y + new_h]).reshape(1, 4)
+        cx, cy, w_norm, h_norm = xyxy2xywhn(bbox, bw, bh)[0]
+        yolo_label_str = f"{yolo_class_id} {cx:.6f} {cy:.6f} {w_norm:.6f} {h_norm:.6f}"
+        saved_paths: List[Path] = []
+        img_output_path = Path(image_target_dir) / f"{overlay_path.stem}{background_path.suffix}"
+        label_output_path = Path(label_target_dir) / f"{overlay_path.stem}.txt"
+        try:
+            Image.fromarray(comp, "RGB").save(img_output_path)
+            saved_paths.append(img_output_path)
+            with open(label_output_path, "w", encoding="utf-8") as f:
+                f.write(yolo_label_str)
+            saved_paths.append(label_output_path)
+            return saved_paths
+        except Exception as e_save:
+            print(f"Erreur {names}: Échec lors de la sauvegarde: {e_save}")
+            for p in saved_paths:
+                try:
+                    if p.exists():
+                        p.unlink()
+                except OSError:
+                    print(f"Avertissement: Impossible de nettoyer le fichier partiellement créé {p}")
+            return None
+
+    return batch_run(arg_tuples, threads, load, compute, save)
+
+
+paste_overlay_onto_background.batch = _overlays_batch

@@ -14,8 +14,9 @@ from typing import List
 
 import numpy as np
 
-from ._common import device_transform
+from ._common import batch_run, device_transform
 from .. import _rt
+from .. import batch_ops as BO
 from .. import device_ccl
 from .. import io as _io
 from ..utils.utils import _validate_dirs
@@ -39,3 +40,41 @@ def keep_largest_component(file: Path, output_dirs: List[Path], min_component_si
     except Exception as e_save:
         print(f"Erreur [{file.name} - Symétrie]: Échec de sauvegarde pour {output_path.name}: {e_save}")
         return None
+
+
+def _keep_batch(arg_tuples, output_dirs: List[Path], threads: int = 1, min_component_size: int = 500,
+                **options) -> List:
+    """Batched keep_largest_component: decode on host threads, one
+    ipp_ccl_keep_largest + one crop launch for the chunk, encode on threads."""
+    output_dir = _validate_dirs(output_dirs, nb_dirs=1)
+
+    def load(args):
+        file = args[0]
+        if file.suffix.lower() != ".png":
+            raise ValueError(f"Le fichier {file.name} n'est pas un PNG.")
+        image = _io.imread(str(file), _io.IMREAD_UNCHANGED)
+        if image is None:
+            raise FileNotFoundError(f"Impossible de charger l'image {file.name}.")
+        if image.shape[2] != 4:   # IndexError for a 2-D image, as the per-file path
+            raise AttributeError(f"L'image {file.name} ne contient pas de canal alpha, elle sera ignorée.")
+        return image
+
+    def compute(images, _args):
+        return BO.keep_largest(images)
+
+    def save(args, _img, cropped):
+        file = args[0]
+        if cropped is None:
+            raise ValueError("aucun pixel non transparent (cv2.boundingRect(None))")
+        output_path = Path(output_dir) / file.name
+        try:
+            _io.imwrite(str(output_path), cropped)
+            return output_path
+        except Exception as e_save:
+            print(f"Erreur [{file.name} - Symétrie]: Échec de sauvegarde pour {output_path.name}: {e_save}")
+            return None
+
+    return batch_run(arg_tuples, threads, load, compute, save)
+
+
+keep_largest_component.batch = _keep_batch

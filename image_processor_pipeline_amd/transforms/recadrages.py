@@ -12,8 +12,9 @@ from typing import Any, List, Optional, Tuple
 import numpy as np
 from PIL import Image
 
-from ._common import device_transform
+from ._common import batch_run, device_transform
 from .. import _rt
+from .. import batch_ops as BO
 from .. import device as D
 from .. import geometry as G
 from .. import io as _io
@@ -57,6 +58,48 @@ def crop_from_border(
     except Exception as e_save:
         print(f"Erreur [{file.name} - Symétrie]: Échec de sauvegarde pour {output_path.name}: {e_save}")
         return None
+
+
+def _crop_batch(arg_tuples, output_dirs: List[Path], threads: int = 1,
+                crop_margins: Tuple[float, float, float, float] = (0, 0, 0, 0), **options: Any) -> List:
+    """Batched crop_from_border: decode + margin checks on host threads, one
+    ipp_copy_window launch for the chunk, encode on host threads."""
+    output_dir = Path(output_dirs[0])
+
+    def load(args):
+        file = args[0]
+        if file.suffix.lower() not in (".jpg", ".jpeg"):
+            raise ValueError(f"Le Fichier {file.name} n'est pas du type JPG.")
+        image = _io.imread(str(file), _io.IMREAD_UNCHANGED)
+        if image is None:
+            raise FileNotFoundError(f"Impossible de charger l'image {file.name}.")
+        height, width = image.shape[:2]
+        t, b = _compute_crop(crop_margins[0], height), _compute_crop(crop_margins[1], height)
+        l, r = _compute_crop(crop_margins[2], width), _compute_crop(crop_margins[3], width)
+        if t + b >= height or l + r >= width:
+            raise ValueError(f"Les marges de rognage sont trop grandes pour l'image {file.name}.")
+        return image, (l, t, width - l - r, height - t - b)
+
+    def compute(items, _args):
+        return BO.copy_windows([im for im, _ in items], [(k, win, 0) for k, (_, win) in enumerate(items)])
+
+    def save(args, _item, cropped):
+        file = args[0]
+        output_path = output_dir / file.name
+        try:
+            if _io.imwrite(str(output_path), cropped):
+                return output_path
+            print(f"Avertissement [{file.name} - Symétrie]: Échec de sauvegarde (imwrite a retourné False) "
+                  f"pour {output_path.name}")
+            return None
+        except Exception as e_save:
+            print(f"Erreur [{file.name} - Symétrie]: Échec de sauvegarde pour {output_path.name}: {e_save}")
+            return None
+
+    return batch_run(arg_tuples, threads, load, compute, save)
+
+
+crop_from_border.batch = _crop_batch
 
 
 @device_transform
