@@ -48,8 +48,9 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096,
-                    help="items per GPU (weak scaling) or in total (strong scaling)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="items per GPU (weak scaling) or in total (strong scaling); default 4096 for pipe5 "
+                         "(config 3), 1024 for rotflip (config 2)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--backgrounds", type=int, default=16)
@@ -247,6 +248,8 @@ def main(argv=None):
     from image_processor_pipeline_amd import fused, device as D
 
     S, K = args.size, args.backgrounds
+    if args.batch is None:
+        args.batch = 1024 if args.workload == "rotflip" else 4096
     per_gpu = args.frames if args.workload == "video4k" else args.batch
     n_global = per_gpu if args.scaling == "strong" else world * per_gpu
     start, stop = fused.shard_range(n_global, rank, world)

@@ -177,56 +177,104 @@ __device__ __forceinline__ int local_of(const Frame& f, int32_t L, int tx, int t
 // 3-channel BGR image (fused chain).
 enum { SRC_ALPHA = 0, SRC_HSV = 1 };
 
+constexpr int NT = 4;            // tiles per labelling block: a 64×128 strip
+constexpr int MAXC = TPX / 4;    // ≤ one 8-connected component per 2×2 block of a tile
+
+// Per-lane source samples of one tile (8 rows of the lane's column): the raw
+// pixel dword (HSV source) or the alpha byte (α source).  Loads of tile t+1 are
+// issued before tile t is labelled, so their latency hides behind its work.
+template <int SRC>
+__device__ __forceinline__ void ccl_load(const uint8_t* __restrict__ img, const ipp_image_desc& d, int x, int ty,
+                                         int wave, uint32_t (&raw)[TH / 4]) {
+#pragma unroll
+    for (int j = 0; j < TH / 4; ++j) {
+        const int y = ty * TH + wave + 4 * j;
+        raw[j] = 0u;
+        if (x < d.w && y < d.h) {
+            const uint8_t* row = img + d.off + (int64_t)y * d.pitch;
+            if (SRC == SRC_ALPHA) {
+                raw[j] = row[4 * x + 3];
+            } else {
+                const bool wide_ok = (y < d.h - 1) || (x < d.w - 1);
+                raw[j] = load_rgb_opaque(row + 3 * x, wide_ok);
+            }
+        }
+    }
+}
+
+// K1: one block labels NT vertically consecutive 64×32 tiles.  Per tile:
+//   A  fg bits per row (ballot) → run labels (each pixel points at its run
+//      start, the run minimum) — no atomics;
+//   B  one LDS union per pair of 8-adjacent runs in consecutive rows;
+//   C  local root of every pixel (run starts walk the forest, the run takes
+//      its start's root by shuffle);
+//   C2 roots get compact ids 0..n-1 (per-component LDS arrays of TPX/4, not
+//      per-pixel ones: 20 KB of LDS per block, 8 blocks per CU);
+//   D  area and row/column masks per component by wave-aggregated LDS
+//      atomics; the uint16 local-root plane; the tile's entry range from one
+//      global atomic whose latency hides behind D;
+//   E  one entry {global root, area, bbox} per component; P[root] = root.
 template <int SRC, int NR, bool ZONES>
 __global__ void __launch_bounds__(256)
 k_ccl_tile(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
            const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, int32_t* __restrict__ counts,
-           int tiles_per_img, int tiles_x_max, ipp_hsv_params hp) {
+           int strips_per_img, int tiles_x_max, ipp_hsv_params hp) {
     constexpr int RPW = TH / 4;  // rows per wave
-    __shared__ int lab[TPX];     // union-find parents; then per root the mask of its rows
-    __shared__ uint32_t area[TPX];
-    __shared__ unsigned long long cols[TPX];  // per root: mask of its columns
+    __shared__ int lab[TPX];     // union-find parents; then, at roots, the component id
+    __shared__ uint32_t c_area[MAXC];
+    __shared__ unsigned long long c_cols[MAXC];
+    __shared__ uint32_t c_rows[MAXC];
+    __shared__ uint16_t c_root[MAXC];
     __shared__ unsigned long long rowbits[TH];
     struct NoTables {};
     __shared__ typename std::conditional<SRC == SRC_HSV, HsvTables<NR>, NoTables>::type T;
     __shared__ int nroots, base;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / tiles_per_img;
-    const int t = b - im * tiles_per_img;
-    const int ty = t / tiles_x_max, tx = t - ty * tiles_x_max;
+    const int im = b / strips_per_img;
+    const int s = b - im * strips_per_img;
+    const int sy = s / tiles_x_max, tx = s - sy * tiles_x_max;
     const ipp_image_desc d = descs[im];
     const Frame f = frame_of(d);
-    if (tx >= f.tiles_x || ty >= f.tiles_y) return;  // block-uniform
+    const int ty0 = sy * NT;
+    if (tx >= f.tiles_x || ty0 >= f.tiles_y) return;  // block-uniform
+    const int ntile = min(NT, f.tiles_y - ty0);
     const Work k = work_of(scratch, works[im]);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = tx * TW + lane;
-    const unsigned long long below = (1ull << lane) - 1ull;
-
+    uint32_t cur[RPW], nxt[RPW];
+    ccl_load<SRC>(img, d, tx * TW + (int)(threadIdx.x & 63), ty0, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+                  cur);
     Ranges<SRC == SRC_HSV ? NR : 1> R;  // zones only (the test itself is table-driven)
     if constexpr (SRC == SRC_HSV) {
         hsv_tables_init<NR>(T, hp);
         if (ZONES) ranges_init<NR, ZONES>(R, hp, d.w, d.h);
-        __syncthreads();
     }
-    if (threadIdx.x == 0) nroots = 0;
 
-    // A. fg bits per row (ballot) and run labels: a run's pixels point at its
-    //    first pixel, whose local index is the run minimum.
-    uint32_t fgmask = 0;
-    int startlane[RPW];
+#pragma unroll 1
+    for (int it = 0; it < ntile; ++it) {
+        // Per-lane values are re-derived every tile from an opaque copy of the
+        // lane id: hoisted out of the loop they would pin ~70 VGPRs for the
+        // whole strip and halve the occupancy.
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int x = tx * TW + lane;
+        const unsigned long long below = (1ull << lane) - 1ull;
+        const int ty = ty0 + it;
+        if (it + 1 < ntile) ccl_load<SRC>(img, d, x, ty + 1, wave, nxt);
+        if (threadIdx.x == 0) nroots = 0;
+        if (SRC == SRC_HSV && it == 0) __syncthreads();  // tables visible
+
+        // A. fg bits per row and run labels.
+        uint32_t fgmask = 0;
+        int startlane[RPW];
 #pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-        const int ly = wave + 4 * j, y = ty * TH + ly;
-        bool fg = false;
-        if (x < d.w && y < d.h) {
-            const uint8_t* row = img + d.off + (int64_t)y * d.pitch;
-            if (SRC == SRC_ALPHA) {
-                fg = row[4 * x + 3] > 1;
-            } else {
-                const bool wide_ok = (y < d.h - 1) || (x < d.w - 1);
-                const uint32_t px = load_rgb_opaque(row + 3 * x, wide_ok);
-                if constexpr (SRC == SRC_HSV) {
-                    uint32_t ex = hsv_tab_excl<NR, true>(T, px);
+        for (int j = 0; j < RPW; ++j) {
+            const int ly = wave + 4 * j, y = ty * TH + ly;
+            bool fg = false;
+            if (x < d.w && y < d.h) {
+                if (SRC == SRC_ALPHA) {
+                    fg = cur[j] > 1u;
+                } else if constexpr (SRC == SRC_HSV) {
+                    uint32_t ex = hsv_tab_excl<NR, true>(T, cur[j]);
                     if (ZONES) {
                         uint32_t zb = 0;
 #pragma unroll
@@ -238,105 +286,114 @@ k_ccl_tile(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ d
                     fg = ex == 0u;
                 }
             }
+            const unsigned long long bits = __ballot(fg);
+            const unsigned long long gaps = ~bits & below;
+            const int start = gaps ? 64 - __clzll(gaps) : 0;
+            startlane[j] = start;
+            lab[lidx(lane, ly)] = fg ? lidx(start, ly) : -1;
+            if (lane == 0) rowbits[ly] = bits;
+            fgmask |= (fg ? 1u : 0u) << j;
         }
-        const unsigned long long bits = __ballot(fg);
-        const unsigned long long gaps = ~bits & below;
-        const int start = gaps ? 64 - __clzll(gaps) : 0;
-        startlane[j] = start;
-        const int li = lidx(lane, ly);
-        lab[li] = fg ? lidx(start, ly) : -1;
-        area[li] = 0u;
-        cols[li] = 0ull;
-        if (lane == 0) rowbits[ly] = bits;
-        fgmask |= (fg ? 1u : 0u) << j;
-    }
-    __syncthreads();
+        __syncthreads();
 
-    // B. one union per pair of 8-adjacent runs in rows ly-1, ly: the run start
-    //    takes the pixels above-left and above; every pixel takes the one
-    //    above-right when that pixel starts a run segment above (its left
-    //    neighbour above is background).
+        // B. one union per pair of 8-adjacent runs in rows ly-1, ly: the run
+        //    start takes the pixels above-left and above; every pixel takes
+        //    the one above-right when it starts a run segment above.
 #pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-        const int ly = wave + 4 * j;
-        if (ly == 0 || !((fgmask >> j) & 1u)) continue;
-        const unsigned long long up = rowbits[ly - 1];
-        const int li = lidx(lane, ly);
-        const bool at_start = lane == 0 || !((rowbits[ly] >> (lane - 1)) & 1ull);
-        const bool u = (up >> lane) & 1ull;
-        if (at_start) {
-            if (lane > 0 && ((up >> (lane - 1)) & 1ull)) lunite(lab, li, lidx(lane - 1, ly - 1));
-            if (u) lunite(lab, li, lidx(lane, ly - 1));
-        }
-        if (lane < TW - 1 && ((up >> (lane + 1)) & 1ull) && !u) lunite(lab, li, lidx(lane + 1, ly - 1));
-    }
-    __syncthreads();
-
-    // C. local root of every pixel (register), root flags: only run starts
-    //    walk the forest; the rest of a run takes its start's root by shuffle.
-    int root[RPW];
-    uint32_t rootmask = 0;
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-        const int li = lidx(lane, wave + 4 * j);
-        const bool fg = (fgmask >> j) & 1u;
-        const int rs = (fg && startlane[j] == lane) ? lfind(lab, li) : 0;
-        const int rr = __shfl(rs, startlane[j]);
-        root[j] = fg ? rr : -1;
-        rootmask |= (root[j] == li ? 1u : 0u) << j;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) lab[lidx(lane, wave + 4 * j)] = 0;  // now: row masks
-    __syncthreads();
-
-    // D. per row, per distinct root in the wave: area and bbox (one set of LDS
-    //    atomics per root, by the lowest lane holding it); lab16 out.
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-        const int ly = wave + 4 * j, y = ty * TH + ly;
-        const bool fg = (fgmask >> j) & 1u;
-        unsigned long long pending = __ballot(fg);
-        while (pending) {
-            const int leader = __ffsll((long long)pending) - 1;
-            const int r = __shfl(root[j], leader);
-            const unsigned long long same = __ballot(root[j] == r) & pending;
-            if (lane == leader) {
-                atomicAdd(&area[r], (uint32_t)__popcll(same));
-                atomicOr(&cols[r], same);
-                atomicOr(reinterpret_cast<unsigned int*>(&lab[r]), 1u << ly);
+        for (int j = 0; j < RPW; ++j) {
+            const int ly = wave + 4 * j;
+            if (ly == 0 || !((fgmask >> j) & 1u)) continue;
+            const unsigned long long up = rowbits[ly - 1];
+            const int li = lidx(lane, ly);
+            const bool at_start = lane == 0 || !((rowbits[ly] >> (lane - 1)) & 1ull);
+            const bool u = (up >> lane) & 1ull;
+            if (at_start) {
+                if (lane > 0 && ((up >> (lane - 1)) & 1ull)) lunite(lab, li, lidx(lane - 1, ly - 1));
+                if (u) lunite(lab, li, lidx(lane, ly - 1));
             }
-            pending &= ~same;
+            if (lane < TW - 1 && ((up >> (lane + 1)) & 1ull) && !u) lunite(lab, li, lidx(lane + 1, ly - 1));
         }
-        if (x < d.w && y < d.h) k.lab16[(int64_t)y * d.w + x] = fg ? (uint16_t)root[j] : NOFG;
-    }
-    __syncthreads();
+        __syncthreads();
 
-    // E. one entry per local component
-    int slot[RPW];
+        // C. local root of every pixel.
+        int root[RPW];
+        uint32_t rootmask = 0;
 #pragma unroll
-    for (int j = 0; j < RPW; ++j) slot[j] = ((rootmask >> j) & 1u) ? atomicAdd(&nroots, 1) : -1;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        base = nroots > 0 ? atomicAdd(&counts[im], nroots) : 0;
-        k.tile[ty * f.tiles_x + tx] = make_int2(base, nroots);
-    }
-    __syncthreads();
-    const int x0 = tx * TW, y0 = ty * TH;
+        for (int j = 0; j < RPW; ++j) {
+            const int li = lidx(lane, wave + 4 * j);
+            const bool fg = (fgmask >> j) & 1u;
+            const int rs = (fg && startlane[j] == lane) ? lfind(lab, li) : 0;
+            const int rr = __shfl(rs, startlane[j]);
+            root[j] = fg ? rr : -1;
+            rootmask |= (root[j] == li ? 1u : 0u) << j;
+        }
+        __syncthreads();
+
+        // C2. compact component ids at the roots.
 #pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-        if (slot[j] < 0) continue;
-        const int ly = wave + 4 * j, li = lidx(lane, ly);
-        const int32_t L = gidx(f, x, y0 + ly);
-        const int e = base + slot[j];
-        k.entL[e] = L;
-        k.entA[e] = area[li];
-        const unsigned long long cm = cols[li];
-        const uint32_t rm = (uint32_t)lab[li];
-        k.entB[e] = make_int4(x0 + __ffsll((long long)cm) - 1, y0 + __ffs((int)rm) - 1, x0 + 64 - __clzll(cm),
-                              y0 + 32 - __clz((int)rm));
-        k.P[L] = L;
-        k.A[L] = 0u;
+        for (int j = 0; j < RPW; ++j) {
+            if (!((rootmask >> j) & 1u)) continue;
+            const int li = lidx(lane, wave + 4 * j);
+            const int c = atomicAdd(&nroots, 1);
+            lab[li] = c;
+            c_root[c] = (uint16_t)li;
+            c_area[c] = 0u;
+            c_cols[c] = 0ull;
+            c_rows[c] = 0u;
+        }
+        __syncthreads();
+
+        // D. per row, per distinct component in the wave: area and bbox masks
+        //    (one set of LDS atomics per component, by its lowest lane);
+        //    the local-root plane; the tile's entry range.
+        int gbase = 0;
+        const int n = nroots;
+        if (threadIdx.x == 0 && n > 0) gbase = atomicAdd(&counts[im], n);
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            const int ly = wave + 4 * j, y = ty * TH + ly;
+            const bool fg = (fgmask >> j) & 1u;
+            const int cid = fg ? lab[root[j]] : -1;
+            unsigned long long pending = __ballot(fg);
+            while (pending) {
+                const int leader = __ffsll((long long)pending) - 1;
+                const int c = __shfl(cid, leader);
+                const unsigned long long same = __ballot(cid == c) & pending;
+                if (lane == leader) {
+                    atomicAdd(&c_area[c], (uint32_t)__popcll(same));
+                    atomicOr(&c_cols[c], same);
+                    atomicOr(&c_rows[c], 1u << ly);
+                }
+                pending &= ~same;
+            }
+            if (x < d.w && y < d.h) k.lab16[(int64_t)y * d.w + x] = fg ? (uint16_t)root[j] : NOFG;
+        }
+        if (threadIdx.x == 0) {
+            base = gbase;
+            k.tile[ty * f.tiles_x + tx] = make_int2(gbase, n);
+        }
+        __syncthreads();
+
+        // E. one entry per component.
+        const int x0 = tx * TW, y0 = ty * TH;
+        for (int c = threadIdx.x; c < n; c += 256) {
+            const int li = c_root[c];
+            int lx, ly;
+            lpos(li, lx, ly);
+            const int32_t L = gidx(f, x0 + lx, y0 + ly);
+            const int e = base + c;
+            k.entL[e] = L;
+            k.entA[e] = c_area[c];
+            const unsigned long long cm = c_cols[c];
+            const uint32_t rm = c_rows[c];
+            k.entB[e] = make_int4(x0 + __ffsll((long long)cm) - 1, y0 + __ffs((int)rm) - 1, x0 + 64 - __clzll(cm),
+                                  y0 + 32 - __clz((int)rm));
+            k.P[L] = L;
+            k.A[L] = 0u;
+        }
+        __syncthreads();  // LDS reused by the next tile
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) cur[j] = nxt[j];
     }
 }
 
@@ -580,9 +637,9 @@ __global__ void k_ccl_finish(int32_t* bbox, int n) {
 }
 
 struct Launch {
-    int tiles_x, tiles_y, tiles_per_img;
+    int tiles_x, tiles_y, tiles_per_img, strips_per_img;
     int border_chunks, ent_chunks;
-    dim3 tile_grid, border_grid, ent_grid;
+    dim3 tile_grid, strip_grid, border_grid, ent_grid;
     bool ok;
 };
 
@@ -591,6 +648,7 @@ Launch plan_launch(int n, int max_w, int max_h, int64_t max_ent) {
     L.tiles_x = (max_w + TW - 1) / TW;
     L.tiles_y = (max_h + TH - 1) / TH;
     L.tiles_per_img = L.tiles_x * L.tiles_y;
+    L.strips_per_img = L.tiles_x * ((L.tiles_y + NT - 1) / NT);
     const int64_t border = (int64_t)(L.tiles_x - 1) * max_h + (int64_t)(L.tiles_y - 1) * max_w;
     L.border_chunks = (int)std::max<int64_t>(1, (border + 255) / 256);
     (void)max_ent;
@@ -598,6 +656,7 @@ Launch plan_launch(int n, int max_w, int max_h, int64_t max_ent) {
     const int64_t tb = (int64_t)L.tiles_per_img * n, bb = (int64_t)L.border_chunks * n, eb = (int64_t)L.ent_chunks * n;
     L.ok = tb < INT32_MAX && bb < INT32_MAX && eb < INT32_MAX;
     L.tile_grid = dim3((uint32_t)tb);
+    L.strip_grid = dim3((uint32_t)((int64_t)L.strips_per_img * n));
     L.border_grid = dim3((uint32_t)bb);
     L.ent_grid = dim3((uint32_t)eb);
     return L;
@@ -606,8 +665,8 @@ Launch plan_launch(int n, int max_w, int max_h, int64_t max_ent) {
 template <int SRC, int NR, bool ZONES>
 void launch_tiles(const Launch& L, hipStream_t s, const uint8_t* img, const ipp_image_desc* descs,
                   const ipp_ccl_work* works, uint8_t* scratch, int32_t* counts, const ipp_hsv_params& hp) {
-    hipLaunchKernelGGL((k_ccl_tile<SRC, NR, ZONES>), L.tile_grid, dim3(256), 0, s, img, descs, works, scratch, counts,
-                       L.tiles_per_img, L.tiles_x, hp);
+    hipLaunchKernelGGL((k_ccl_tile<SRC, NR, ZONES>), L.strip_grid, dim3(256), 0, s, img, descs, works, scratch,
+                       counts, L.strips_per_img, L.tiles_x, hp);
 }
 
 // K1..K5 common to both entry points.

@@ -48,12 +48,12 @@ def main():
         wk = [k for k in write if sym(k)]
         if not fk or not wk:
             continue
-        fv = [v for k in fk for v in fetch[k].values()]
-        wv = [v for k in wk for v in write[k].values()]
-        f_bytes = 2 * 1024 * sum(fv) / len(fv)
-        w_bytes = 1024 * sum(wv) / len(wv)
+        # one entry point may launch several kernels (ipp_video_keep_largest):
+        # per kernel the mean over its dispatches, summed over the kernels
+        f_bytes = 2 * 1024 * sum(sum(fetch[k].values()) / len(fetch[k]) for k in fk)
+        w_bytes = 1024 * sum(sum(write[k].values()) / len(write[k]) for k in wk)
         res[api] = {"hbm_bytes": int(f_bytes + w_bytes), "fetch_bytes_x2": int(f_bytes), "write_bytes": int(w_bytes),
-                    "dispatches": len(fv)}
+                    "kernels": len(fk), "dispatches": sum(len(fetch[k]) for k in fk)}
     data = json.load(open(out)) if os.path.exists(out) else {}
     data[workload] = res
     json.dump(data, open(out, "w"), indent=1)
