@@ -37,7 +37,16 @@ $(LIB): $(OBJS)
 asm: | $(OBJDIR)
 	for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) -S --cuda-device-only $$f -o $(OBJDIR)/$$(basename $$f .hip).s; done
 
+# Experiment builds (A/B on the GPU box through IPP_LIB_PATH): one in-tree
+# library per variant, variants/<name>/libipp.so, built with VFLAGS.
+#   make variant NAME=fill VFLAGS=-DIPP_HP_FILL_SKIP
+variant:
+	mkdir -p variants/$(NAME)/obj
+	for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) $(VFLAGS) $$( [ "$$(basename $$f)" = ipp_bilinear.hip -o "$$(basename $$f)" = ipp_enhance.hip ] && echo -ffp-contract=off ) -c $$f -o variants/$(NAME)/obj/$$(basename $$f .hip).o || exit 1; done
+	g++ $(HOSTFLAGS) -c $(CSRC)/ipp_host.cpp -o variants/$(NAME)/obj/ipp_host.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o variants/$(NAME)/libipp.so variants/$(NAME)/obj/*.o -lpthread
+
 clean:
 	rm -rf build $(LIB)
 
-.PHONY: all clean asm
+.PHONY: all clean asm variant

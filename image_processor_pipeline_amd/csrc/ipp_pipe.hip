@@ -82,17 +82,22 @@ typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 //     h + 32 falls out of the rounding constant (2048 + 32·4096), and hm folds
 //     OpenCV's h < 0 → h + 180 wrap into the table.
 // ---------------------------------------------------------------------------
-template <int NR>
+// BANDS: 16-row bands per block (256 threads each).  Bands of one block are
+// consecutive rows of one item and sweep the same columns in lockstep, so
+// their source gathers and tap tiles share the CU's L1.
+typedef uint8_t WinRing[4][HR][WSTRIDE];   // planar window ring, bytes p ^ 0x80
+
+template <int NR, int BANDS = 1>
 struct __attribute__((aligned(16))) Hpass2Lds {
     typedef typename MaskType<NR>::T MT;
-    uint8_t win[4][HR][WSTRIDE];   // planar window ring, bytes p ^ 0x80
+    WinRing win[BANDS];
     HsvTables<NR> T;               // table-driven HSV test (ipp_hsv.h)
 };
 
 // M pixel → window byte quad (p | α 255) ^ 0x80 when kept, 0x80808080 (transparent black) when excluded.
 template <int NR, bool ZONES>
-__device__ __forceinline__ uint32_t hsv2_px(const Hpass2Lds<NR>& L, uint32_t raw, uint32_t zbits) {
-    uint32_t ex = hsv_tab_excl<NR, false>(L.T, raw);
+__device__ __forceinline__ uint32_t hsv2_px(const HsvTables<NR>& T, uint32_t raw, uint32_t zbits) {
+    uint32_t ex = hsv_tab_excl<NR, false>(T, raw);
     if (ZONES) ex &= zbits;
     const uint32_t t = (raw | 0xFF000000u) ^ 0x80808080u;
     return ex ? 0x80808080u : t;
@@ -174,12 +179,12 @@ __device__ __forceinline__ Hp2Chunk hp2_chunk(const int4* hdr, int s0, int ntile
 }
 
 template <int NR, bool ZONES, int CN, bool CLAMP, int DBG = 0>
-__device__ __forceinline__ void hpass2_body(Hpass2Lds<NR>& L, const Hp2Block& B, uint8_t* __restrict__ tmp,
+__device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win, int wave, const Hp2Block& B,
+                                            uint8_t* __restrict__ tmp,
                                             const int32_t* __restrict__ coefs, const ipp_resample_desc& h,
                                             int row0, int nrows, const int32_t* zc0, const int32_t* zcw,
                                             uint32_t zrow, uint32_t fill) {
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = lane >> 2;
     const int ntiles = (h.out_len + 15) >> 4;
     const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
@@ -214,7 +219,7 @@ __device__ __forceinline__ void hpass2_body(Hpass2Lds<NR>& L, const Hp2Block& B,
     for (;;) {
         // This wave's tile taps for the first K step, in flight during phase 1.
         const int t = ck.s0 + wave;
-        const bool has_tile = !(DBG & 4) && t < ck.s1;
+        const bool has_tile = !(DBG & 4) && t < ck.s1 && nrows > 0;
         int4 th = make_int4(0, 0, 0, 0);
         uint4 bn[3];
         const uint4* bt = tblk + lane;
@@ -251,12 +256,12 @@ __device__ __forceinline__ void hpass2_body(Hpass2Lds<NR>& L, const Hp2Block& B,
                 for (int k = 0; k < 4; ++k) {
                     uint32_t raw = P.p[k];
                     if (CLAMP) raw >>= P.sh[k];
-                    px[k] = (DBG & 2) ? (raw | 0x80808080u) : hsv2_px<NR, ZONES>(L, raw, zb[k]);
+                    px[k] = (DBG & 2) ? (raw | 0x80808080u) : hsv2_px<NR, ZONES>(T, raw, zb[k]);
                 }
                 transpose4(px[0], px[1], px[2], px[3], ch);
             } else if (ZONES) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) px[k] = hsv2_px<NR, ZONES>(L, 0u, zb[k]);
+                for (int k = 0; k < 4; ++k) px[k] = hsv2_px<NR, ZONES>(T, 0u, zb[k]);
                 transpose4(px[0], px[1], px[2], px[3], ch);
             } else {
 #pragma unroll
@@ -265,7 +270,7 @@ __device__ __forceinline__ void hpass2_body(Hpass2Lds<NR>& L, const Hp2Block& B,
             if (active) {
                 const int pos = x & (RING - 1);
 #pragma unroll
-                for (int c = 0; c < 4; ++c) *reinterpret_cast<uint32_t*>(&L.win[c][r][pos]) = ch[c];
+                for (int c = 0; c < 4; ++c) *reinterpret_cast<uint32_t*>(&win[c][r][pos]) = ch[c];
             }
         };
         for (int st = 0; st < nsteps; st += 3) {
@@ -315,7 +320,7 @@ __device__ __forceinline__ void hpass2_body(Hpass2Lds<NR>& L, const Hp2Block& B,
                 const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const i32x4 a = *reinterpret_cast<const i32x4*>(&L.win[c][arow][pos]);
+                    const i32x4 a = *reinterpret_cast<const i32x4*>(&win[c][arow][pos]);
 #pragma unroll
                     for (int p = 0; p < 3; ++p)
                         acc[c][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[p], acc[c][p], 0, 0, 0);
@@ -354,6 +359,7 @@ __device__ __forceinline__ void paste_bands(const ipp_paste_desc& p, int& vb0, i
     vb1 = max(vb1, vb0);
 }
 
+template <int NT = 256>
 __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, const uint8_t* __restrict__ bg,
                                                       uint8_t* __restrict__ dst, int share, int nshare) {
     int vb0, vb1;
@@ -371,16 +377,16 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4* s4 = reinterpret_cast<const u32x4*>(sb);
         u32x4* d4 = reinterpret_cast<u32x4*>(db);
-        for (int64_t i0 = a + threadIdx.x; i0 < e; i0 += 8 * 256) {
+        for (int64_t i0 = a + threadIdx.x; i0 < e; i0 += 8 * NT) {
             u32x4 v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int64_t i = i0 + 256 * j;
+                const int64_t i = i0 + NT * j;
                 if (i < e) v[j] = s4[i < n0 ? i : i + skip];
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int64_t i = i0 + 256 * j;
+                const int64_t i = i0 + NT * j;
                 if (i < e) __builtin_nontemporal_store(v[j], d4 + (i < n0 ? i : i + skip));
             }
         }
@@ -394,7 +400,7 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
         const int y = rr < vb0 ? rr : rr - vb0 + vb1;
         const uint8_t* brow = sb + (int64_t)y * p.bg_pitch;
         uint8_t* drow = db + (int64_t)y * p.dst_pitch;
-        for (int ci = threadIdx.x; ci < chunks; ci += 256) {
+        for (int ci = threadIdx.x; ci < chunks; ci += NT) {
             const int c0 = ci << 4, nb = min(16, rb - c0);
             const bool vec = nb == 16 && ((reinterpret_cast<uintptr_t>(brow + c0) | reinterpret_cast<uintptr_t>(drow + c0)) & 15u) == 0;
             uint32_t w[4];
@@ -404,29 +410,39 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
     }
 }
 
-template <int NR, bool ZONES, int CN, int DBG = 0, bool COPY = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+#ifndef IPP_HP_WAVES
+#define IPP_HP_WAVES 4
+#endif
+#ifndef IPP_HP_BANDS
+#define IPP_HP_BANDS 1
+#endif
+template <int NR, bool ZONES, int CN, int DBG = 0, bool COPY = false, int BANDS = IPP_HP_BANDS>
+__global__ void __launch_bounds__(256 * BANDS) __attribute__((amdgpu_waves_per_eu(IPP_HP_WAVES)))
 k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
               const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp, const uint8_t* __restrict__ bg,
               uint8_t* __restrict__ dst, int cpi) {
-    __shared__ Hpass2Lds<NR> L;
+    __shared__ Hpass2Lds<NR, BANDS> L;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    // COPY: each item owns tiles_y H-pass blocks followed by cpi background-copy
-    // blocks, so copies run beside the VALU-bound H pass on every XCD.
+    // tiles_y = H-pass blocks per item (BANDS bands each).  COPY: each item
+    // owns tiles_y H-pass blocks followed by cpi background-copy blocks, so
+    // copies run beside the VALU-bound H pass on every XCD.
     const int per_item = tiles_y + (COPY ? cpi : 0);
     const int im = b / per_item;
-    const int ty = b - im * per_item;
-    if (COPY && ty >= tiles_y) {
-        bg_copy_outside_bands(descs[im].p, bg, dst, ty - tiles_y, cpi);
+    const int tb = b - im * per_item;
+    if (COPY && tb >= tiles_y) {
+        bg_copy_outside_bands<256 * BANDS>(descs[im].p, bg, dst, tb - tiles_y, cpi);
         return;
     }
     const ipp_gather_desc g = descs[im].g;
     const ipp_resample_desc h = descs[im].h;
-    const int row0 = ty * HR;
-    if (row0 >= h.lines) return;  // block-uniform
+    if (tb * BANDS * HR >= h.lines) return;  // block-uniform
+    const int band = BANDS == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+    const int wib = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);  // wave in the band
+    const int row0 = (tb * BANDS + band) * HR;
+    const bool band_on = row0 < h.lines;  // idle bands keep to the block's barriers
 
-    // Tables (one entry per thread, hm: 192 entries).
-    hsv_tables_init<NR>(L.T, hp);
+    // Tables (one entry per thread of the first 256, hm: 192 entries).
+    if (threadIdx.x < 256) hsv_tables_init<NR>(L.T, hp);
 
     // Zones: per-lane row bits now, column bits per pixel.
     int32_t zc0[ZONES ? NR : 1], zcw[ZONES ? NR : 1];
@@ -490,16 +506,22 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
         }
         B.xlo = (DBG & 8) ? -0x3FFFFFFF : blo;
         B.xhi = (DBG & 8) ? 0x3FFFFFFF : bhi;
+        if (!band_on) {  // no gathers, no rows
+            B.xlo = 0x3FFFFFFF;
+            B.xhi = -0x3FFFFFFF;
+        }
     }
 
     __syncthreads();  // tables visible
     // Fill value (raw 0): uniform over the block except for zone bits.
-    const uint32_t fill = hsv2_px<NR, ZONES>(L, 0u, ~0u);
-    const int nrows = min(HR, h.lines - row0);
+    const uint32_t fill = hsv2_px<NR, ZONES>(L.T, 0u, ~0u);
+    const int nrows = band_on ? min(HR, h.lines - row0) : 0;
     if (CN == 3 && clamp)
-        hpass2_body<NR, ZONES, CN, true, DBG>(L, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+        hpass2_body<NR, ZONES, CN, true, DBG>(L.T, L.win[band], wib, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow,
+                                              fill);
     else
-        hpass2_body<NR, ZONES, CN, false, DBG>(L, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+        hpass2_body<NR, ZONES, CN, false, DBG>(L.T, L.win[band], wib, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow,
+                                               fill);
 
 }
 
@@ -633,11 +655,14 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
 template <int NR, bool ZONES, int CN>
 void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                   const ipp_pipe_desc* descs, int ty, const ipp_hsv_params& hp, const uint8_t* bg, uint8_t* dst) {
+    constexpr int BANDS = IPP_HP_BANDS;
+    const int n = grid.x / ty;
+    const int tyb = (ty + BANDS - 1) / BANDS;  // H-pass blocks per item
     if (bg && dst) {  // H pass + the background rows outside the overlay bands
-        const int cpi = copy_blocks_per_item();
-        const dim3 g2((uint32_t)(grid.x / ty * (ty + cpi)));
-        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 0, true>), g2, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp,
-                           bg, dst, cpi);
+        const int cpi = BANDS == 1 ? copy_blocks_per_item() : 1;
+        const dim3 g2((uint32_t)(n * (tyb + cpi)));
+        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 0, true>), g2, dim3(256 * BANDS), 0, s, src, tmp, coefs, descs,
+                           tyb, hp, bg, dst, cpi);
         return;
     }
 #ifdef IPP_DIAG
@@ -648,7 +673,7 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
     if (dbg >= 10 && NR == 4 && !ZONES && CN == 3) {
         switch (dbg - 10) {
 #define IPP_DIAG_CASE(D) \
-    case D: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, D>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); return;
+    case D: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, D, false, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); return;
             IPP_DIAG_CASE(1) IPP_DIAG_CASE(2) IPP_DIAG_CASE(3) IPP_DIAG_CASE(4) IPP_DIAG_CASE(5) IPP_DIAG_CASE(6)
             IPP_DIAG_CASE(7) IPP_DIAG_CASE(8) IPP_DIAG_CASE(16) IPP_DIAG_CASE(20)
 #undef IPP_DIAG_CASE
@@ -656,7 +681,8 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
         }
     }
 #endif
-    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0);
+    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), dim3((uint32_t)(n * tyb)), dim3(256 * BANDS), 0, s, src, tmp,
+                       coefs, descs, tyb, hp, bg, dst, 0);
 }
 
 template <int NR>

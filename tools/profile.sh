@@ -17,8 +17,10 @@ pmc() { local name=$1; shift; run $name --kernel-include-regex "$FILTER" --pmc "
 run kt --kernel-trace --stats || exit 11
 find $OUT/kt -name '*kernel_trace.csv' -delete
 [ -n "$KT_ONLY" ] && exit 0
+if [ -z "$SQ_ONLY" ]; then
 pmc fetch FETCH_SIZE || exit 12
 pmc write WRITE_SIZE || exit 13
+fi
 pmc sqa SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY || exit 14
 pmc sqb SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_LDS SQ_INSTS_SALU || exit 15
 pmc misc GRBM_GUI_ACTIVE GRBM_TA_BUSY TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum SQ_LDS_UNALIGNED_STALL SQ_LDS_ADDR_CONFLICT || exit 16
