@@ -204,8 +204,10 @@ typedef struct ipp_pipe_desc {
     ipp_paste_desc p;       /* paste: ov = V-pass result (never stored)        */
 } ipp_pipe_desc;
 
-/* H tap formats of ipp_pipe_hpass (ipp_plan_pipe_axes transposed = 1 / 2). */
-#define IPP_TAPS_DOT4 0   /* per-output dot4 planes, v_dot4 on the VALU       */
+/* Tap formats (ipp_plan_pipe_axes transposed = 0/1 / 2 + phase).  The pipe
+ * kernels take IPP_TAPS_MFMA only; any other value returns IPP_E_ARG.  The
+ * dot4 format stays a host planning format (ipp_plan_dot4_*). */
+#define IPP_TAPS_DOT4 0   /* per-output dot4 planes (host planner only)       */
 #define IPP_TAPS_MFMA 1   /* 16-output tiles, v_mfma_i32_16x16x64_i8          */
 
 /* src_cn: channels of every source in the batch (3 or 4); hsv: HOST pointer.
@@ -218,10 +220,9 @@ int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                    const ipp_pipe_desc* descs, int32_t n_images,
                    int32_t max_out_w, int32_t max_rows, int32_t src_cn,
                    const ipp_hsv_params* hsv, int32_t tap_format, void* stream);
-/* tap_format: IPP_TAPS_DOT4 (V axes planned with transposed = 0) or
- * IPP_TAPS_MFMA (V axes planned with transposed = 2 + (p.y mod 16), i.e. tap
- * tiles aligned with 16-row background bands); max_ov_w bounds the overlay
- * widths (MFMA path). */
+/* tap_format: IPP_TAPS_MFMA (V axes planned with transposed = 2 + (p.y mod
+ * 16), i.e. tap tiles aligned with 16-row background bands); max_ov_w bounds
+ * the overlay widths. */
 int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
                     const int32_t* coefs, const ipp_pipe_desc* descs, int32_t n_images,
                     int32_t bg_w, int32_t bg_h, int32_t max_ov_w, int32_t tap_format,
