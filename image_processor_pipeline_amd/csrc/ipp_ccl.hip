@@ -7,47 +7,62 @@
 // (when there is no foreground at all, label 0 — the background — is "kept"
 // and α is left unchanged); :74-81 crop-fit to the bbox of α ≠ 0.
 //
-// Component identity.  Pixel (x, y) has the BLOCK-RASTER index
-//   L = ((y >> 1) * wb + (x >> 1)) * 4 + (y & 1) * 2 + (x & 1),  wb = ⌈w/2⌉,
-// and every union links the larger index under the smaller, so a component's
-// root is its minimum L: root >> 2 is the first 2×2 scan block (blocks in
+// Component identity.  A horizontal run of fg pixels starting at (x, y) has
+// the RUN-START index
+//   G = (((y >> 1) * wb + (x >> 1)) << 1) + (y & 1),  wb = ⌈w/2⌉,
+// unique because two run starts of one row are ≥ 2 columns apart (tile
+// borders are at even columns).  A component's pixel of minimum block-raster
+// order ((y>>1, x>>1), then y&1, x&1) is always a run start, and G orders run
+// starts exactly that way, so every union links the larger G under the
+// smaller and a component's root is the first 2×2 scan block (blocks in
 // raster order) that touches it — the order in which OpenCV's block-based
 // 8-connectivity labelling (Spaghetti/BBDT) numbers components.  The tie rule
 // is therefore "smallest root" (restated; UNPINNED: OpenCV is absent here).
 //
-// Algorithm (tile-local labelling, then border merging):
-//   K1 k_ccl_tile     one 64×32 tile per block, one wave per row: fg bits
-//                     (α > 1, or the fused HSV mask) by ballot → horizontal
-//                     runs labelled without atomics (run start = highest
-//                     clear bit below the lane) → one LDS union per pair of
-//                     8-adjacent runs in consecutive rows → per-pixel local
-//                     root (uint16, raster) → per-component area and row /
-//                     column masks (bbox) by wave-aggregated LDS atomics →
-//                     one entry per local
-//                     component {global root, area, bbox}; P[root] = root.
-//   K2 k_ccl_border   unites the local roots of 8-adjacent fg pixel pairs
-//                     straddling a tile border, skipping pairs a neighbouring
-//                     border pixel already unites (global atomicMin
-//                     union-find on P, touched only at local roots).
-//   K3 k_ccl_resolve  per entry: R = find(P, L); A[R] += area; P[L] = R.
-//   K4 k_ccl_best     per global root: atomicMax of (area << 32 | ~root).
-//   K5 k_ccl_bbox     per entry of the best component: bbox atomics.
-//   K6 k_ccl_emit     per tile meeting the output: flags of its local roots
-//                     (in the best component?) in LDS, then per pixel α := 0
-//                     outside it in place (plugin path), or the crop-fit
-//                     written as BGRA from the BGR frame (fused chain).
+// Algorithm (bit-plane runs; one wave per 64×64 tile, lane = row):
+//   K1 k_ccl_label   fg bit per pixel (α > 1, or the fused HSV mask), one
+//                    ballot per row → the row's 64-bit mask word in lane r.
+//                    Runs come from the word (start = m & ~(m << 1)); each
+//                    run unites, through a per-wave LDS union-find over run
+//                    slots, with the runs of row r-1 it touches (8-adjacency:
+//                    columns a-1 .. b+1).  Compact component ids by a wave
+//                    scan; area / row and column masks per component by LDS
+//                    atomics in passes of MAXC ids; one entry per component
+//                    {global root G, area, bbox}; P[G] = G.  Written per
+//                    tile: the 64 mask words (tile-major), the global root of
+//                    every edge pixel (top, bottom, left, right; -1 for
+//                    background), (first entry, count).  No per-pixel label
+//                    plane: 1 bit per pixel plus 1 KB per tile.
+//   K2 k_ccl_border  unites the roots of 8-adjacent fg pixel pairs straddling
+//                    a tile border (edge arrays), skipping pairs a neighbouring
+//                    border pixel already unites (global atomicMin union-find
+//                    on P, touched only at roots).
+//   K3 k_ccl_resolve per entry: R = find(P, G); A[R] += area; P[G] = R.
+//   K4 k_ccl_best    per global root: atomicMax of (area << 32 | ~root).
+//   K5 k_ccl_bbox    per entry of the best component: bbox atomics.
+//   K6 k_ccl_emit    per tile meeting the output: which of its components are
+//                    in the best one (entries); a tile whose components are
+//                    all in (or all out) takes its mask words (or nothing); a
+//                    mixed tile relabels its mask words (the same
+//                    deterministic labelling as K1, so the same ids).  Then
+//                    α := 0 outside the component in place (plugin path), or
+//                    the crop-fit written as BGRA from the BGR frame (fused
+//                    chain).
 // Pixels are read once in K1 and once in K6 (within the crop for the fused
-// chain); everything else is per component.
+// chain); everything else is per run, per component or per edge pixel.
 #include <algorithm>
-
 #include <type_traits>
 
 #include "ipp_hsv.h"
 
 namespace {
 
-constexpr int TW = 64, TH = 32, TPX = TW * TH;  // tile (2048 pixels)
-constexpr uint16_t NOFG = 0xFFFF;
+constexpr int TW = 64, TH = 64;        // tile: one wave, lane r owns row r
+constexpr int NJ = (TW / 2) * TH;      // run-start slots per tile (row, column pair)
+constexpr int MAXC = 32;               // component stats per LDS pass
+constexpr int CMAX = (TW / 2) * (TH / 2);  // ≤ one 8-connected component per 2×2 block
+constexpr int WAVES = 4;               // tiles (waves) per block
+typedef unsigned long long u64;
 
 struct Frame {
     int w, h, wb, tiles_x, tiles_y;
@@ -63,25 +78,33 @@ __device__ __forceinline__ Frame frame_of(const ipp_image_desc& d) {
     return f;
 }
 
-__device__ __forceinline__ int32_t gidx(const Frame& f, int x, int y) {
-    return (((y >> 1) * f.wb + (x >> 1)) << 2) + ((y & 1) << 1) + (x & 1);
+// Run-start slot inside a tile; orders slots as G orders run starts.
+__device__ __forceinline__ int slot(int r, int a) { return ((((r >> 1) << 5) + (a >> 1)) << 1) | (r & 1); }
+
+// Global run-start index of slot j of tile (tx, ty).
+__device__ __forceinline__ int32_t slot_gidx(const Frame& f, int tx, int ty, int j) {
+    const int r = ((j >> 6) << 1) | (j & 1);
+    const int y = ty * TH + r;
+    return (((y >> 1) * f.wb + tx * (TW / 2) + ((j >> 1) & 31)) << 1) + (y & 1);
 }
 
-// Local (in-tile) index with the same ordering as gidx among the tile's pixels.
-__device__ __forceinline__ int lidx(int lx, int ly) {
-    return (((ly >> 1) * (TW / 2) + (lx >> 1)) << 2) + ((ly & 1) << 1) + (lx & 1);
-}
-__device__ __forceinline__ void lpos(int li, int& lx, int& ly) {
-    const int blk = li >> 2;
-    ly = ((blk / (TW / 2)) << 1) + ((li >> 1) & 1);
-    lx = ((blk % (TW / 2)) << 1) + (li & 1);
+__device__ __forceinline__ int ctz64(u64 v) { return __ffsll((long long)v) - 1; }
+
+// Calls fn(a, len) for every run of word m (a = first column).
+template <class F>
+__device__ __forceinline__ void for_runs(u64 m, F fn) {
+    u64 s = m & ~(m << 1);
+    while (s) {
+        const int a = ctz64(s);
+        const u64 rest = ~m >> a;
+        const int len = rest ? ctz64(rest) : 64 - a;
+        fn(a, len);
+        s &= s - 1;
+    }
 }
 
-// Global index of the local root `lr` of tile (tx, ty).
-__device__ __forceinline__ int32_t root_gidx(const Frame& f, int tx, int ty, int lr) {
-    int lx, ly;
-    lpos(lr, lx, ly);
-    return gidx(f, tx * TW + lx, ty * TH + ly);
+__device__ __forceinline__ u64 run_mask(int a, int len) {
+    return (len >= 64 ? ~0ull : ((1ull << len) - 1ull)) << a;
 }
 
 __device__ __forceinline__ int32_t ld(const int32_t* p) {
@@ -114,48 +137,123 @@ __device__ __forceinline__ void gunite(int32_t* P, int32_t a, int32_t b) {
 }
 
 __device__ __forceinline__ int lld(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
-__device__ __forceinline__ int lfind(const int* lab, int x) {
-    int p = lld(lab + x);
+__device__ __forceinline__ int lfind(const int* par, int x) {
+    int p = lld(par + x);
     while (p != x) {
         x = p;
-        p = lld(lab + x);
+        p = lld(par + x);
     }
     return x;
 }
 
-__device__ __forceinline__ void lunite(int* lab, int a, int b) {
+__device__ __forceinline__ void lunite(int* par, int a, int b) {
     for (;;) {
-        a = lfind(lab, a);
-        b = lfind(lab, b);
+        a = lfind(par, a);
+        b = lfind(par, b);
         if (a == b) return;
         if (a > b) {
             const int t = a;
             a = b;
             b = t;
         }
-        const int old = atomicMin(lab + b, a);
+        const int old = __hip_atomic_fetch_min(par + b, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         if (old == b) return;
         b = old;
     }
 }
 
+// LDS writes of one lane become visible to the other lanes of its wave.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave-wide exclusive prefix sum of v (and the total).
+__device__ __forceinline__ int wave_scan_excl(int v, int lane, int& total) {
+    int s = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(s, o);
+        if (lane >= o) s += t;
+    }
+    total = __shfl(s, 63);
+    return s - v;
+}
+
+// Tile labelling on the mask words (lane r: word m of row r, p of row r-1).
+// On return par[slot] holds, for a root run, NJ + its component id, and for
+// any other run its root's slot; returns the component count.  Component ids
+// follow (row, run) order — a pure function of the words, so K6 relabelling a
+// tile reproduces K1's ids.
+__device__ __forceinline__ int label_tile(int* par, int r, int lane, u64 m, u64 p) {
+    for_runs(m, [&](int a, int) { par[slot(r, a)] = slot(r, a); });
+    wave_sync();
+    if (p) {
+        const u64 ps = p & ~(p << 1);
+        for_runs(m, [&](int a, int len) {
+            const int me = slot(r, a);
+            if (a > 0 && ((p >> (a - 1)) & 1ull)) {
+                // the run of row r-1 covering column a-1 starts at the highest
+                // start ≤ a-1
+                const u64 below = ps & ((a >= 64 ? ~0ull : ((1ull << a) - 1ull)));
+                lunite(par, me, slot(r - 1, 63 - __clzll(below)));
+            }
+            const int hi = min(a + len, 63);  // columns a .. b+1
+            u64 hit = ps & (((hi >= 63 ? ~0ull : ((2ull << hi) - 1ull))) & ~((1ull << a) - 1ull));
+            while (hit) {
+                lunite(par, me, slot(r - 1, ctz64(hit)));
+                hit &= hit - 1;
+            }
+        });
+    }
+    wave_sync();
+    int nroot = 0;
+    for_runs(m, [&](int a, int) {
+        const int j = slot(r, a);
+        const int root = lfind(par, j);
+        nroot += root == j;
+        if (root != j) par[j] = root;
+    });
+    wave_sync();
+    int n;
+    int cid = wave_scan_excl(nroot, lane, n);
+    for_runs(m, [&](int a, int) {
+        const int j = slot(r, a);
+        if (par[j] == j) par[j] = NJ + cid++;
+    });
+    wave_sync();
+    return n;
+}
+
+__device__ __forceinline__ int run_root(const int* par, int j) {
+    const int v = par[j];
+    return v >= NJ ? j : v;
+}
+__device__ __forceinline__ int run_cid(const int* par, int j) {
+    const int v = par[j];
+    return (v >= NJ ? v : par[v]) - NJ;
+}
+
 // Scratch layout per image (offsets in the ipp_ccl_work descriptor).
 struct Work {
-    uint16_t* lab16;   // w*h local roots (raster); NOFG for background
-    int32_t* P;        // 4*wb*hb parent array (touched at local roots only)
-    uint32_t* A;       // 4*wb*hb areas (touched at roots only)
-    int32_t* entL;     // per local component: global root index
-    uint32_t* entA;    // ... its in-tile area
-    int4* entB;        // ... its bbox (x0, y0, x1, y1), image coordinates
-    int2* tile;        // per tile: (first entry, entry count)
+    u64* mask;        // per tile 64 row words (tile-major)
+    int32_t* edge;    // per tile 4 × 64 edge roots: top, bottom, left, right
+    int32_t* P;       // 2*wb*hb parent array (touched at run-start roots only)
+    uint32_t* A;      // 2*wb*hb areas (touched at roots only)
+    int32_t* entL;    // per local component: global root index
+    uint32_t* entA;   // ... its in-tile area
+    int4* entB;       // ... its bbox (x0, y0, x1, y1), image coordinates
+    int2* tile;       // per tile: (first entry, entry count)
 };
 
 __device__ __forceinline__ Work work_of(uint8_t* scratch, const ipp_ccl_work& w) {
     Work k;
-    k.lab16 = reinterpret_cast<uint16_t*>(scratch + w.lab_off);
+    k.mask = reinterpret_cast<u64*>(scratch + w.mask_off);
+    k.edge = reinterpret_cast<int32_t*>(scratch + w.edge_off);
     k.P = reinterpret_cast<int32_t*>(scratch + w.p_off);
     k.A = reinterpret_cast<uint32_t*>(scratch + w.a_off);
     k.entL = reinterpret_cast<int32_t*>(scratch + w.ent_off);
@@ -165,248 +263,208 @@ __device__ __forceinline__ Work work_of(uint8_t* scratch, const ipp_ccl_work& w)
     return k;
 }
 
-// Local index of the pixel with global block-raster index L inside tile (tx, ty).
-__device__ __forceinline__ int local_of(const Frame& f, int32_t L, int tx, int ty) {
-    const int32_t blk = L >> 2;
-    const int by = blk / f.wb, bx = blk - by * f.wb;
-    const int y = 2 * by + ((L >> 1) & 1), x = 2 * bx + (L & 1);
-    return lidx(x - tx * TW, y - ty * TH);
-}
+enum { E_TOP = 0, E_BOT = 1, E_LEFT = 2, E_RIGHT = 3 };
 
 // Foreground source: α > 1 of a 4-channel image, or the HSV mask of a
 // 3-channel BGR image (fused chain).
 enum { SRC_ALPHA = 0, SRC_HSV = 1 };
 
-constexpr int NT = 4;            // tiles per labelling block: a 64×128 strip
-constexpr int MAXC = TPX / 4;    // ≤ one 8-connected component per 2×2 block of a tile
+constexpr int RB = 16;  // rows per load batch (double-buffered)
 
-// Per-lane source samples of one tile (8 rows of the lane's column): the raw
-// pixel dword (HSV source) or the alpha byte (α source).  Loads of tile t+1 are
-// issued before tile t is labelled, so their latency hides behind its work.
-template <int SRC>
-__device__ __forceinline__ void ccl_load(const uint8_t* __restrict__ img, const ipp_image_desc& d, int x, int ty,
-                                         int wave, uint32_t (&raw)[TH / 4]) {
+// Source samples of RB rows of the lane's column: the raw pixel dword (HSV
+// source) or the alpha byte (α source).  FULL: every row is inside the image
+// and not its last one, every column inside the image (no checks; a 4-byte
+// read at the row's last pixel stays inside the next row).
+template <int SRC, bool FULL>
+__device__ __forceinline__ void load_rows(const uint8_t* __restrict__ img, const ipp_image_desc& d, int x, int y0,
+                                          uint32_t (&raw)[RB]) {
+    const uint8_t* base = img + d.off + (int64_t)y0 * d.pitch + (SRC == SRC_ALPHA ? 4 * x + 3 : 3 * x);
 #pragma unroll
-    for (int j = 0; j < TH / 4; ++j) {
-        const int y = ty * TH + wave + 4 * j;
-        raw[j] = 0u;
-        if (x < d.w && y < d.h) {
-            const uint8_t* row = img + d.off + (int64_t)y * d.pitch;
-            if (SRC == SRC_ALPHA) {
-                raw[j] = row[4 * x + 3];
-            } else {
-                const bool wide_ok = (y < d.h - 1) || (x < d.w - 1);
-                raw[j] = load_rgb_opaque(row + 3 * x, wide_ok);
+    for (int k = 0; k < RB; ++k) {
+        const uint8_t* p = base + (int64_t)k * d.pitch;
+        if (FULL) {
+            raw[k] = SRC == SRC_ALPHA ? (uint32_t)*p : ld_u32_unaligned(p);
+        } else {
+            const int y = y0 + k;
+            raw[k] = 0u;
+            if (x < d.w && y < d.h) {
+                if (SRC == SRC_ALPHA) raw[k] = *p;
+                else raw[k] = load_rgb_opaque(p, (y < d.h - 1) || (x < d.w - 1));
             }
         }
     }
 }
 
-// K1: one block labels NT vertically consecutive 64×32 tiles.  Per tile:
-//   A  fg bits per row (ballot) → run labels (each pixel points at its run
-//      start, the run minimum) — no atomics;
-//   B  one LDS union per pair of 8-adjacent runs in consecutive rows;
-//   C  local root of every pixel (run starts walk the forest, the run takes
-//      its start's root by shuffle);
-//   C2 roots get compact ids 0..n-1 (per-component LDS arrays of TPX/4, not
-//      per-pixel ones: 20 KB of LDS per block, 8 blocks per CU);
-//   D  area and row/column masks per component by wave-aggregated LDS
-//      atomics; the uint16 local-root plane; the tile's entry range from one
-//      global atomic whose latency hides behind D;
-//   E  one entry {global root, area, bbox} per component; P[root] = root.
+// Mask words of one tile: lane = column while loading; lane r returns row r's
+// word in m and row r-1's in p.
+template <int SRC, int NR, bool ZONES, bool FULL>
+__device__ __forceinline__ void tile_words(const uint8_t* __restrict__ img, const ipp_image_desc& d, int x, int y0,
+                                           int lane, const HsvTables<NR>* T, const Ranges<NR>& R, u64& m, u64& p) {
+    uint32_t zx = 0;  // ranges whose zone columns hold this lane's column
+    if constexpr (SRC == SRC_HSV && ZONES) {
+#pragma unroll
+        for (int q = 0; q < NR; ++q) zx |= (uint32_t)((uint32_t)(x - R.c0[q]) < (uint32_t)R.cw[q]) << q;
+    }
+    const bool xin = x < d.w;
+    m = 0ull;
+    p = 0ull;
+    uint32_t bufA[RB], bufB[RB];
+    load_rows<SRC, FULL>(img, d, x, y0, bufA);
+#pragma unroll
+    for (int rb = 0; rb < TH / RB; ++rb) {
+        uint32_t(&cur)[RB] = (rb & 1) ? bufB : bufA;
+        uint32_t(&nxt)[RB] = (rb & 1) ? bufA : bufB;
+        if (rb + 1 < TH / RB) load_rows<SRC, FULL>(img, d, x, y0 + (rb + 1) * RB, nxt);
+#pragma unroll
+        for (int kk = 0; kk < RB; ++kk) {
+            const int r = rb * RB + kk, y = y0 + r;
+            bool fg;
+            if constexpr (SRC == SRC_ALPHA) {
+                fg = cur[kk] > 1u;
+            } else {
+                uint32_t ex = hsv_tab_excl<NR, true>(*T, cur[kk]);
+                if (ZONES) {
+                    uint32_t zy = 0;
+#pragma unroll
+                    for (int q = 0; q < NR; ++q) zy |= (uint32_t)((uint32_t)(y - R.r0[q]) < (uint32_t)R.rh[q]) << q;
+                    ex &= zx & zy;
+                }
+                fg = ex == 0u;
+            }
+            if (!FULL) fg = fg && xin && y < d.h;
+            const u64 bits = __ballot(fg);
+            m = lane == r ? bits : m;
+            p = lane == r + 1 ? bits : p;
+        }
+    }
+}
+
+// K1: one wave per 64×64 tile, WAVES tiles side by side per block.
 template <int SRC, int NR, bool ZONES>
-__global__ void __launch_bounds__(256)
-k_ccl_tile(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
-           const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, int32_t* __restrict__ counts,
-           int strips_per_img, int tiles_x_max, ipp_hsv_params hp) {
-    constexpr int RPW = TH / 4;  // rows per wave
-    __shared__ int lab[TPX];     // union-find parents; then, at roots, the component id
-    __shared__ uint32_t c_area[MAXC];
-    __shared__ unsigned long long c_cols[MAXC];
-    __shared__ uint32_t c_rows[MAXC];
-    __shared__ uint16_t c_root[MAXC];
-    __shared__ unsigned long long rowbits[TH];
+__global__ void __launch_bounds__(64 * WAVES)
+k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
+            const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, int32_t* __restrict__ counts,
+            int groups_per_img, int groups_x, ipp_hsv_params hp) {
+    __shared__ int par_s[WAVES][NJ];
+    __shared__ uint32_t st_area[WAVES][MAXC];
+    __shared__ u64 st_rows[WAVES][MAXC], st_cols[WAVES][MAXC];
     struct NoTables {};
     __shared__ typename std::conditional<SRC == SRC_HSV, HsvTables<NR>, NoTables>::type T;
-    __shared__ int nroots, base;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / strips_per_img;
-    const int s = b - im * strips_per_img;
-    const int sy = s / tiles_x_max, tx = s - sy * tiles_x_max;
+    const int im = b / groups_per_img;
+    const int g = b - im * groups_per_img;
+    const int ty = g / groups_x;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int tx = (g - ty * groups_x) * WAVES + wave;
     const ipp_image_desc d = descs[im];
     const Frame f = frame_of(d);
-    const int ty0 = sy * NT;
-    if (tx >= f.tiles_x || ty0 >= f.tiles_y) return;  // block-uniform
-    const int ntile = min(NT, f.tiles_y - ty0);
-    const Work k = work_of(scratch, works[im]);
-    uint32_t cur[RPW], nxt[RPW];
-    ccl_load<SRC>(img, d, tx * TW + (int)(threadIdx.x & 63), ty0, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
-                  cur);
-    Ranges<SRC == SRC_HSV ? NR : 1> R;  // zones only (the test itself is table-driven)
+    Ranges<NR> R;  // zones only (the test itself is table-driven)
     if constexpr (SRC == SRC_HSV) {
         hsv_tables_init<NR>(T, hp);
         if (ZONES) ranges_init<NR, ZONES>(R, hp, d.w, d.h);
+        __syncthreads();
+    }
+    if (tx >= f.tiles_x || ty >= f.tiles_y) return;  // wave-uniform; no barrier follows
+    int* par = par_s[wave];
+    const Work k = work_of(scratch, works[im]);
+    const int x = tx * TW + lane, y0 = ty * TH;
+
+    // A. mask words.
+    u64 m, p;
+    const HsvTables<NR>* Tp = nullptr;
+    if constexpr (SRC == SRC_HSV) Tp = &T;
+    if (tx * TW + TW <= d.w && y0 + TH < d.h)
+        tile_words<SRC, NR, ZONES, true>(img, d, x, y0, lane, Tp, R, m, p);
+    else
+        tile_words<SRC, NR, ZONES, false>(img, d, x, y0, lane, Tp, R, m, p);
+    k.mask[(int64_t)(ty * f.tiles_x + tx) * TH + lane] = m;
+
+    // B-F. runs, unions, component ids.
+    const int r = lane;
+    const int n = label_tile(par, r, lane, m, p);
+    int base = 0;
+    if (lane == 0 && n > 0) base = atomicAdd(&counts[im], n);
+    base = __shfl(base, 0);
+    if (lane == 0) k.tile[ty * f.tiles_x + tx] = make_int2(base, n);
+
+    // Entries: roots write the global root; P / A initialised there.
+    for_runs(m, [&](int a, int) {
+        const int j = slot(r, a);
+        const int v = par[j];
+        if (v >= NJ) {
+            const int32_t G = slot_gidx(f, tx, ty, j);
+            k.entL[base + v - NJ] = G;
+            k.P[G] = G;
+            k.A[G] = 0u;
+        }
+    });
+
+    // Stats per component, MAXC ids per pass.
+    uint32_t* area = st_area[wave];
+    u64* rows = st_rows[wave];
+    u64* cols = st_cols[wave];
+    for (int c0 = 0; c0 < n; c0 += MAXC) {
+        if (lane < MAXC) {
+            area[lane] = 0u;
+            rows[lane] = 0ull;
+            cols[lane] = 0ull;
+        }
+        wave_sync();
+        for_runs(m, [&](int a, int len) {
+            const int c = run_cid(par, slot(r, a)) - c0;
+            if ((unsigned)c < (unsigned)MAXC) {
+                atomicAdd(&area[c], (uint32_t)len);
+                atomicOr(&rows[c], 1ull << r);
+                atomicOr(&cols[c], run_mask(a, len));
+            }
+        });
+        wave_sync();
+        if (lane < MAXC && c0 + lane < n) {
+            const int e = base + c0 + lane;
+            const u64 cm = cols[lane], rm = rows[lane];
+            const int X0 = tx * TW;
+            k.entA[e] = area[lane];
+            k.entB[e] = make_int4(X0 + ctz64(cm), y0 + ctz64(rm), X0 + 64 - __clzll(cm), y0 + 64 - __clzll(rm));
+        }
+        wave_sync();
     }
 
-#pragma unroll 1
-    for (int it = 0; it < ntile; ++it) {
-        // Per-lane values are re-derived every tile from an opaque copy of the
-        // lane id: hoisted out of the loop they would pin ~70 VGPRs for the
-        // whole strip and halve the occupancy.
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-        const int x = tx * TW + lane;
-        const unsigned long long below = (1ull << lane) - 1ull;
-        const int ty = ty0 + it;
-        if (it + 1 < ntile) ccl_load<SRC>(img, d, x, ty + 1, wave, nxt);
-        if (threadIdx.x == 0) nroots = 0;
-        if (SRC == SRC_HSV && it == 0) __syncthreads();  // tables visible
-
-        // A. fg bits per row and run labels.
-        uint32_t fgmask = 0;
-        int startlane[RPW];
-#pragma unroll
-        for (int j = 0; j < RPW; ++j) {
-            const int ly = wave + 4 * j, y = ty * TH + ly;
-            bool fg = false;
-            if (x < d.w && y < d.h) {
-                if (SRC == SRC_ALPHA) {
-                    fg = cur[j] > 1u;
-                } else if constexpr (SRC == SRC_HSV) {
-                    uint32_t ex = hsv_tab_excl<NR, true>(T, cur[j]);
-                    if (ZONES) {
-                        uint32_t zb = 0;
-#pragma unroll
-                        for (int q = 0; q < NR; ++q)
-                            zb |= (uint32_t)(((uint32_t)(y - R.r0[q]) < (uint32_t)R.rh[q]) &
-                                             ((uint32_t)(x - R.c0[q]) < (uint32_t)R.cw[q])) << q;
-                        ex &= zb;
-                    }
-                    fg = ex == 0u;
-                }
-            }
-            const unsigned long long bits = __ballot(fg);
-            const unsigned long long gaps = ~bits & below;
-            const int start = gaps ? 64 - __clzll(gaps) : 0;
-            startlane[j] = start;
-            lab[lidx(lane, ly)] = fg ? lidx(start, ly) : -1;
-            if (lane == 0) rowbits[ly] = bits;
-            fgmask |= (fg ? 1u : 0u) << j;
+    // Edge roots (global G of the pixel's root, -1 for background).
+    int32_t* edge = k.edge + (int64_t)(ty * f.tiles_x + tx) * (4 * 64);
+    {
+        const u64 s = m & ~(m << 1);
+        // left / right: lane r's own row
+        edge[E_LEFT * 64 + lane] = (m & 1ull) ? slot_gidx(f, tx, ty, run_root(par, slot(r, 0))) : -1;
+        edge[E_RIGHT * 64 + lane] =
+            (m >> 63) ? slot_gidx(f, tx, ty, run_root(par, slot(r, 63 - __clzll(s)))) : -1;
+        // top / bottom: lane = column of rows 0 and 63
+        const u64 m0 = __shfl(m, 0), m63 = __shfl(m, TH - 1);
+        const u64 upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+        int32_t t = -1, bo = -1;
+        if ((m0 >> lane) & 1ull) {
+            const u64 s0 = m0 & ~(m0 << 1) & upto;
+            t = slot_gidx(f, tx, ty, run_root(par, slot(0, 63 - __clzll(s0))));
         }
-        __syncthreads();
-
-        // B. one union per pair of 8-adjacent runs in rows ly-1, ly: the run
-        //    start takes the pixels above-left and above; every pixel takes
-        //    the one above-right when it starts a run segment above.
-#pragma unroll
-        for (int j = 0; j < RPW; ++j) {
-            const int ly = wave + 4 * j;
-            if (ly == 0 || !((fgmask >> j) & 1u)) continue;
-            const unsigned long long up = rowbits[ly - 1];
-            const int li = lidx(lane, ly);
-            const bool at_start = lane == 0 || !((rowbits[ly] >> (lane - 1)) & 1ull);
-            const bool u = (up >> lane) & 1ull;
-            if (at_start) {
-                if (lane > 0 && ((up >> (lane - 1)) & 1ull)) lunite(lab, li, lidx(lane - 1, ly - 1));
-                if (u) lunite(lab, li, lidx(lane, ly - 1));
-            }
-            if (lane < TW - 1 && ((up >> (lane + 1)) & 1ull) && !u) lunite(lab, li, lidx(lane + 1, ly - 1));
+        if ((m63 >> lane) & 1ull) {
+            const u64 s63 = m63 & ~(m63 << 1) & upto;
+            bo = slot_gidx(f, tx, ty, run_root(par, slot(TH - 1, 63 - __clzll(s63))));
         }
-        __syncthreads();
-
-        // C. local root of every pixel.
-        int root[RPW];
-        uint32_t rootmask = 0;
-#pragma unroll
-        for (int j = 0; j < RPW; ++j) {
-            const int li = lidx(lane, wave + 4 * j);
-            const bool fg = (fgmask >> j) & 1u;
-            const int rs = (fg && startlane[j] == lane) ? lfind(lab, li) : 0;
-            const int rr = __shfl(rs, startlane[j]);
-            root[j] = fg ? rr : -1;
-            rootmask |= (root[j] == li ? 1u : 0u) << j;
-        }
-        __syncthreads();
-
-        // C2. compact component ids at the roots.
-#pragma unroll
-        for (int j = 0; j < RPW; ++j) {
-            if (!((rootmask >> j) & 1u)) continue;
-            const int li = lidx(lane, wave + 4 * j);
-            const int c = atomicAdd(&nroots, 1);
-            lab[li] = c;
-            c_root[c] = (uint16_t)li;
-            c_area[c] = 0u;
-            c_cols[c] = 0ull;
-            c_rows[c] = 0u;
-        }
-        __syncthreads();
-
-        // D. per row, per distinct component in the wave: area and bbox masks
-        //    (one set of LDS atomics per component, by its lowest lane);
-        //    the local-root plane; the tile's entry range.
-        int gbase = 0;
-        const int n = nroots;
-        if (threadIdx.x == 0 && n > 0) gbase = atomicAdd(&counts[im], n);
-#pragma unroll
-        for (int j = 0; j < RPW; ++j) {
-            const int ly = wave + 4 * j, y = ty * TH + ly;
-            const bool fg = (fgmask >> j) & 1u;
-            const int cid = fg ? lab[root[j]] : -1;
-            unsigned long long pending = __ballot(fg);
-            while (pending) {
-                const int leader = __ffsll((long long)pending) - 1;
-                const int c = __shfl(cid, leader);
-                const unsigned long long same = __ballot(cid == c) & pending;
-                if (lane == leader) {
-                    atomicAdd(&c_area[c], (uint32_t)__popcll(same));
-                    atomicOr(&c_cols[c], same);
-                    atomicOr(&c_rows[c], 1u << ly);
-                }
-                pending &= ~same;
-            }
-            if (x < d.w && y < d.h) k.lab16[(int64_t)y * d.w + x] = fg ? (uint16_t)root[j] : NOFG;
-        }
-        if (threadIdx.x == 0) {
-            base = gbase;
-            k.tile[ty * f.tiles_x + tx] = make_int2(gbase, n);
-        }
-        __syncthreads();
-
-        // E. one entry per component.
-        const int x0 = tx * TW, y0 = ty * TH;
-        for (int c = threadIdx.x; c < n; c += 256) {
-            const int li = c_root[c];
-            int lx, ly;
-            lpos(li, lx, ly);
-            const int32_t L = gidx(f, x0 + lx, y0 + ly);
-            const int e = base + c;
-            k.entL[e] = L;
-            k.entA[e] = c_area[c];
-            const unsigned long long cm = c_cols[c];
-            const uint32_t rm = c_rows[c];
-            k.entB[e] = make_int4(x0 + __ffsll((long long)cm) - 1, y0 + __ffs((int)rm) - 1, x0 + 64 - __clzll(cm),
-                                  y0 + 32 - __clz((int)rm));
-            k.P[L] = L;
-            k.A[L] = 0u;
-        }
-        __syncthreads();  // LDS reused by the next tile
-#pragma unroll
-        for (int j = 0; j < RPW; ++j) cur[j] = nxt[j];
+        edge[E_TOP * 64 + lane] = t;
+        edge[E_BOT * 64 + lane] = bo;
     }
 }
 
-// Pixel (x, y) of tile-local root → global root index, or -1 for background.
-__device__ __forceinline__ int32_t root_of(const Frame& f, const Work& k, int x, int y) {
-    const uint16_t r = k.lab16[(int64_t)y * f.w + x];
-    if (r == NOFG) return -1;
-    return root_gidx(f, x / TW, y / TH, r);
+// Root of pixel (x, y) on a tile edge, from that tile's edge array.
+__device__ __forceinline__ int32_t edge_root(const Frame& f, const Work& k, int x, int y, int which) {
+    const int tx = x / TW, ty = y / TH;
+    const int i = (which == E_LEFT || which == E_RIGHT) ? (y - ty * TH) : (x - tx * TW);
+    return k.edge[(int64_t)(ty * f.tiles_x + tx) * (4 * 64) + which * 64 + i];
 }
 
 // Border pairs.  Thread i < vert owns left pixel (64*bx - 1, y) of a vertical
 // tile border and its 8-neighbours (64*bx, y-1..y+1); the rest own the upper
-// pixel (x, 32*by - 1) of a horizontal border and (x-1..x+1, 32*by).  Along a
+// pixel (x, 64*by - 1) of a horizontal border and (x-1..x+1, 64*by).  Along a
 // border, consecutive owners usually see the same pair of roots: a pair is
 // skipped when the previous (next) owner with the same near-side root takes
 // it, so a long shared boundary costs one union, not one per pixel.
@@ -421,27 +479,30 @@ k_ccl_border(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __res
     const Work k = work_of(scratch, works[im]);
     const int64_t vert = (int64_t)(f.tiles_x - 1) * f.h;
     const int64_t horz = (int64_t)(f.tiles_y - 1) * f.w;
-    // near side pixel (nx, ny) moving along the border by (sx, sy); far side at +(fx, fy)
-    int nx, ny, sx, sy, fx, fy, pos, len;
+    int nx, ny, sx, sy, fx, fy, pos, len, near_e, far_e;
     if (i < vert) {
         const int bx = 1 + (int)(i / f.h);
         pos = (int)(i % f.h);
         len = f.h;
         nx = bx * TW - 1, ny = pos, sx = 0, sy = 1, fx = 1, fy = 0;
+        near_e = E_RIGHT, far_e = E_LEFT;
     } else if (i < vert + horz) {
         const int64_t j = i - vert;
         const int by = 1 + (int)(j / f.w);
         pos = (int)(j % f.w);
         len = f.w;
         nx = pos, ny = by * TH - 1, sx = 1, sy = 0, fx = 0, fy = 1;
+        near_e = E_BOT, far_e = E_TOP;
     } else {
         return;
     }
-    const int32_t a = root_of(f, k, nx, ny);
+    const int32_t a = edge_root(f, k, nx, ny, near_e);
     if (a < 0) return;
-    auto near_at = [&](int p) { return (p < 0 || p >= len) ? -1 : root_of(f, k, nx + (p - pos) * sx, ny + (p - pos) * sy); };
-    auto far_at = [&](int p) {
-        return (p < 0 || p >= len) ? -1 : root_of(f, k, nx + fx + (p - pos) * sx, ny + fy + (p - pos) * sy);
+    auto near_at = [&](int q) {
+        return (q < 0 || q >= len) ? -1 : edge_root(f, k, nx + (q - pos) * sx, ny + (q - pos) * sy, near_e);
+    };
+    auto far_at = [&](int q) {
+        return (q < 0 || q >= len) ? -1 : edge_root(f, k, nx + fx + (q - pos) * sx, ny + fy + (q - pos) * sy, far_e);
     };
     const int32_t ap = near_at(pos - 1), an = near_at(pos + 1);
     const int32_t cp = far_at(pos - 1), c0 = far_at(pos), cn = far_at(pos + 1);
@@ -528,21 +589,46 @@ k_ccl_bbox(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch
     }
 }
 
-// Flags (LDS) of a tile's local roots: in the best component?  Returns false
-// when the tile has no pixel of it.
-__device__ __forceinline__ bool tile_flags(const Frame& f, const Work& k, int tx, int ty, int32_t broot,
-                                           uint8_t* flag, int* any) {
-    const int2 te = k.tile[ty * f.tiles_x + tx];
-    if (threadIdx.x == 0) *any = 0;
+// K6 front half (one block per tile): the tile's row words restricted to
+// the best component, into inw[64].  Every thread of the block takes part.
+struct EmitLds {
+    u64 inw[TH];
+    uint8_t flag[CMAX];
+    int par[NJ];
+    int any;  // bit 0: a component in the best one, bit 1: one outside it
+};
+
+__device__ __forceinline__ void tile_in_words(const Frame& f, const Work& k, int tx, int ty, int32_t broot,
+                                              EmitLds& L) {
+    const int tile = ty * f.tiles_x + tx;
+    const int2 te = k.tile[tile];
+    if (threadIdx.x == 0) L.any = 0;
     __syncthreads();
-    for (int e = threadIdx.x; e < te.y; e += 256) {
-        const int32_t L = k.entL[te.x + e];
-        const bool in = k.P[L] == broot;
-        flag[local_of(f, L, tx, ty)] = in ? 1 : 0;
-        if (in) *any = 1;
+    int any = 0;
+    for (int e = threadIdx.x; e < te.y; e += blockDim.x) {
+        const bool in = k.P[k.entL[te.x + e]] == broot;
+        L.flag[e] = in ? 1 : 0;
+        any |= in ? 1 : 2;
+    }
+    if (any) atomicOr(&L.any, any);
+    __syncthreads();
+    const int mode = L.any;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        const u64 m = k.mask[(int64_t)tile * TH + lane];
+        u64 w = 0ull;
+        if (mode == 1) {
+            w = m;
+        } else if (mode == 3) {
+            const u64 p = __shfl_up(m, 1);
+            label_tile(L.par, lane, lane, m, lane > 0 ? p : 0ull);
+            for_runs(m, [&](int a, int len) {
+                if (L.flag[run_cid(L.par, slot(lane, a))]) w |= run_mask(a, len);
+            });
+        }
+        L.inw[lane] = w;
     }
     __syncthreads();
-    return *any != 0;
 }
 
 // K6, plugin path: in place on a 4-channel image, α := 0 outside the best
@@ -551,8 +637,7 @@ __global__ void __launch_bounds__(256)
 k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
             uint8_t* __restrict__ scratch, const unsigned long long* __restrict__ best, int tiles_per_img,
             int tiles_x_max) {
-    __shared__ uint8_t flag[TPX];
-    __shared__ int any;
+    __shared__ EmitLds L;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int im = b / tiles_per_img;
     const int t = b - im * tiles_per_img;
@@ -563,15 +648,14 @@ k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
     const int32_t broot = best_root(best[im]);
     if (broot < 0) return;
     const Work k = work_of(scratch, works[im]);
-    tile_flags(f, k, tx, ty, broot, flag, &any);
+    tile_in_words(f, k, tx, ty, broot, L);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = tx * TW + lane;
     if (x >= d.w) return;
-    for (int j = 0; j < TH / 4; ++j) {
-        const int y = ty * TH + wave + 4 * j;
+    for (int r = wave; r < TH; r += 4) {
+        const int y = ty * TH + r;
         if (y >= d.h) break;
-        const uint16_t r = k.lab16[(int64_t)y * d.w + x];
-        if (r == NOFG || !flag[r]) {
+        if (!((L.inw[r] >> lane) & 1ull)) {
             uint8_t* a = img + d.off + (int64_t)y * d.pitch + 4 * (int64_t)x + 3;
             if (*a) *a = 0;
         }
@@ -587,8 +671,7 @@ k_ccl_crop_bgr(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict
                const unsigned long long* __restrict__ best, const int32_t* __restrict__ bbox,
                uint8_t* __restrict__ out, const ipp_image_desc* __restrict__ out_descs, int tiles_per_img,
                int tiles_x_max) {
-    __shared__ uint8_t flag[TPX];
-    __shared__ int any;
+    __shared__ EmitLds L;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int im = b / tiles_per_img;
     const int t = b - im * tiles_per_img;
@@ -601,19 +684,18 @@ k_ccl_crop_bgr(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict
     const int bx0 = bbox[4 * im + 0], by0 = bbox[4 * im + 1], bx1 = bbox[4 * im + 2], by1 = bbox[4 * im + 3];
     if (tx * TW >= bx1 || (tx + 1) * TW <= bx0 || ty * TH >= by1 || (ty + 1) * TH <= by0) return;
     const Work k = work_of(scratch, works[im]);
-    tile_flags(f, k, tx, ty, broot, flag, &any);
+    tile_in_words(f, k, tx, ty, broot, L);
     const ipp_image_desc od = out_descs[im];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = tx * TW + lane;
     if (x < bx0 || x >= bx1) return;
-    for (int j = 0; j < TH / 4; ++j) {
-        const int y = ty * TH + wave + 4 * j;
-        if (y < by0) continue;
+    const int r0 = max(wave, by0 - ty * TH + ((wave - (by0 - ty * TH)) & 3));
+    for (int r = r0; r < TH; r += 4) {
+        const int y = ty * TH + r;
         if (y >= by1) break;
         const bool wide_ok = (y < d.h - 1) || (x < d.w - 1);
         const uint32_t px = load_rgb_opaque(img + d.off + (int64_t)y * d.pitch + 3 * (int64_t)x, wide_ok);
-        const uint16_t r = k.lab16[(int64_t)y * d.w + x];
-        const bool in = r != NOFG && flag[r];
+        const bool in = (L.inw[r] >> lane) & 1ull;
         reinterpret_cast<uint32_t*>(out + od.off + (int64_t)(y - by0) * od.pitch)[x - bx0] =
             (px & 0x00FFFFFFu) | (in ? 0xFF000000u : 0u);
     }
@@ -637,56 +719,57 @@ __global__ void k_ccl_finish(int32_t* bbox, int n) {
 }
 
 struct Launch {
-    int tiles_x, tiles_y, tiles_per_img, strips_per_img;
+    int tiles_x, tiles_y, tiles_per_img, groups_x, groups_per_img;
     int border_chunks, ent_chunks;
-    dim3 tile_grid, strip_grid, border_grid, ent_grid;
+    dim3 tile_grid, group_grid, border_grid, ent_grid;
     bool ok;
 };
 
-Launch plan_launch(int n, int max_w, int max_h, int64_t max_ent) {
+Launch plan_launch(int n, int max_w, int max_h) {
     Launch L{};
     L.tiles_x = (max_w + TW - 1) / TW;
     L.tiles_y = (max_h + TH - 1) / TH;
     L.tiles_per_img = L.tiles_x * L.tiles_y;
-    L.strips_per_img = L.tiles_x * ((L.tiles_y + NT - 1) / NT);
+    L.groups_x = (L.tiles_x + WAVES - 1) / WAVES;
+    L.groups_per_img = L.groups_x * L.tiles_y;
     const int64_t border = (int64_t)(L.tiles_x - 1) * max_h + (int64_t)(L.tiles_y - 1) * max_w;
     L.border_chunks = (int)std::max<int64_t>(1, (border + 255) / 256);
-    (void)max_ent;
     L.ent_chunks = ENT_BLOCKS;
-    const int64_t tb = (int64_t)L.tiles_per_img * n, bb = (int64_t)L.border_chunks * n, eb = (int64_t)L.ent_chunks * n;
-    L.ok = tb < INT32_MAX && bb < INT32_MAX && eb < INT32_MAX;
+    const int64_t tb = (int64_t)L.tiles_per_img * n, gb = (int64_t)L.groups_per_img * n,
+                  bb = (int64_t)L.border_chunks * n, eb = (int64_t)L.ent_chunks * n;
+    L.ok = tb < INT32_MAX && gb < INT32_MAX && bb < INT32_MAX && eb < INT32_MAX;
     L.tile_grid = dim3((uint32_t)tb);
-    L.strip_grid = dim3((uint32_t)((int64_t)L.strips_per_img * n));
+    L.group_grid = dim3((uint32_t)gb);
     L.border_grid = dim3((uint32_t)bb);
     L.ent_grid = dim3((uint32_t)eb);
     return L;
 }
 
 template <int SRC, int NR, bool ZONES>
-void launch_tiles(const Launch& L, hipStream_t s, const uint8_t* img, const ipp_image_desc* descs,
+void launch_label(const Launch& L, hipStream_t s, const uint8_t* img, const ipp_image_desc* descs,
                   const ipp_ccl_work* works, uint8_t* scratch, int32_t* counts, const ipp_hsv_params& hp) {
-    hipLaunchKernelGGL((k_ccl_tile<SRC, NR, ZONES>), L.strip_grid, dim3(256), 0, s, img, descs, works, scratch,
-                       counts, L.strips_per_img, L.tiles_x, hp);
+    hipLaunchKernelGGL((k_ccl_label<SRC, NR, ZONES>), L.group_grid, dim3(64 * WAVES), 0, s, img, descs, works,
+                       scratch, counts, L.groups_per_img, L.groups_x, hp);
 }
 
 // K1..K5 common to both entry points.
 int run_labels(int src, const uint8_t* img, const ipp_image_desc* descs, int32_t n, int32_t max_w, int32_t max_h,
-               const ipp_hsv_params* hsv, const ipp_ccl_work* works, uint8_t* scratch, int64_t max_ent,
-               int32_t* counts, unsigned long long* best, int32_t* bbox, hipStream_t s, Launch& L) {
-    L = plan_launch(n, max_w, max_h, max_ent);
+               const ipp_hsv_params* hsv, const ipp_ccl_work* works, uint8_t* scratch, int32_t* counts,
+               unsigned long long* best, int32_t* bbox, hipStream_t s, Launch& L) {
+    L = plan_launch(n, max_w, max_h);
     if (!L.ok) return IPP_E_ARG;
     const int nb = (n + 255) / 256;
     hipLaunchKernelGGL(k_ccl_prep, dim3(nb), dim3(256), 0, s, bbox, best, counts, n);
     if (src == SRC_ALPHA) {
-        launch_tiles<SRC_ALPHA, 1, false>(L, s, img, descs, works, scratch, counts, ipp_hsv_params{});
+        launch_label<SRC_ALPHA, 1, false>(L, s, img, descs, works, scratch, counts, ipp_hsv_params{});
     } else {
         const bool zones = hsv_has_zones(*hsv);
         const bool small = hsv->n_ranges <= 4;
         const ipp_hsv_params q = hsv_pad(*hsv, small ? 4 : IPP_MAX_HSV_RANGES);
-        if (small && !zones) launch_tiles<SRC_HSV, 4, false>(L, s, img, descs, works, scratch, counts, q);
-        else if (small) launch_tiles<SRC_HSV, 4, true>(L, s, img, descs, works, scratch, counts, q);
-        else if (!zones) launch_tiles<SRC_HSV, IPP_MAX_HSV_RANGES, false>(L, s, img, descs, works, scratch, counts, q);
-        else launch_tiles<SRC_HSV, IPP_MAX_HSV_RANGES, true>(L, s, img, descs, works, scratch, counts, q);
+        if (small && !zones) launch_label<SRC_HSV, 4, false>(L, s, img, descs, works, scratch, counts, q);
+        else if (small) launch_label<SRC_HSV, 4, true>(L, s, img, descs, works, scratch, counts, q);
+        else if (!zones) launch_label<SRC_HSV, IPP_MAX_HSV_RANGES, false>(L, s, img, descs, works, scratch, counts, q);
+        else launch_label<SRC_HSV, IPP_MAX_HSV_RANGES, true>(L, s, img, descs, works, scratch, counts, q);
     }
     hipLaunchKernelGGL(k_ccl_border, L.border_grid, dim3(256), 0, s, descs, works, scratch, L.border_chunks);
     hipLaunchKernelGGL(k_ccl_resolve, L.ent_grid, dim3(256), 0, s, works, scratch, counts);
@@ -700,15 +783,15 @@ int run_labels(int src, const uint8_t* img, const ipp_image_desc* descs, int32_t
 extern "C" int64_t ipp_ccl_scratch_layout(int32_t w, int32_t h, ipp_ccl_work* work) {
     if (w <= 0 || h <= 0) return IPP_E_ARG;
     const int64_t wb = (w + 1) / 2, hb = (h + 1) / 2;
-    const int64_t slots = 4 * wb * hb;
+    const int64_t slots = 2 * wb * hb;
     if (slots >= INT32_MAX) return IPP_E_RANGE;
-    // ≤ one component per 2×2 block of a tile (8-connectivity), per tile
     const int64_t tiles = (int64_t)((w + TW - 1) / TW) * ((h + TH - 1) / TH);
-    const int64_t cap = tiles * (TPX / 4);
+    const int64_t cap = tiles * CMAX;
     auto al = [](int64_t v) { return (v + 255) & ~(int64_t)255; };
     ipp_ccl_work k{};
-    k.lab_off = 0;
-    k.p_off = al(2 * (int64_t)w * h);
+    k.mask_off = 0;
+    k.edge_off = al(8 * TH * tiles);
+    k.p_off = k.edge_off + al(4 * 4 * 64 * tiles);
     k.a_off = k.p_off + al(4 * slots);
     k.ent_off = k.a_off + al(4 * slots);
     k.ent_cap = cap;
@@ -728,8 +811,8 @@ extern "C" int ipp_ccl_keep_largest(uint8_t* img, const ipp_image_desc* descs, i
     hipStream_t s = (hipStream_t)stream;
     unsigned long long* best = reinterpret_cast<unsigned long long*>(stats);
     Launch L;
-    const int rc = run_labels(SRC_ALPHA, img, descs, n_images, max_w, max_h, nullptr, works, scratch, max_ent, counts,
-                              best, bbox, s, L);
+    const int rc =
+        run_labels(SRC_ALPHA, img, descs, n_images, max_w, max_h, nullptr, works, scratch, counts, best, bbox, s, L);
     if (rc != IPP_OK) return rc;
     hipLaunchKernelGGL(k_ccl_apply, L.tile_grid, dim3(256), 0, s, img, descs, works, scratch, best, L.tiles_per_img,
                        L.tiles_x);
@@ -751,8 +834,8 @@ extern "C" int ipp_video_keep_largest(const uint8_t* frames, const ipp_image_des
     hipStream_t s = (hipStream_t)stream;
     unsigned long long* best = reinterpret_cast<unsigned long long*>(stats);
     Launch L;
-    const int rc = run_labels(SRC_HSV, frames, descs, n_images, max_w, max_h, hsv, works, scratch, max_ent, counts,
-                              best, bbox, s, L);
+    const int rc =
+        run_labels(SRC_HSV, frames, descs, n_images, max_w, max_h, hsv, works, scratch, counts, best, bbox, s, L);
     if (rc != IPP_OK) return rc;
     hipLaunchKernelGGL(k_ccl_crop_bgr, L.tile_grid, dim3(256), 0, s, frames, descs, works, scratch, best, bbox, out,
                        out_descs, L.tiles_per_img, L.tiles_x);

@@ -3,8 +3,8 @@
 Reference: transforms/pixels_isolés.py:29-61 (threshold α > 1, 8-connected
 components, keep the largest — lowest label on ties —, α := 0 elsewhere) and
 :74-81 (crop to the bbox of α ≠ 0; cv2.boundingRect(None) raises when no pixel
-is left).  All work runs in libipp.so (ipp_ccl_keep_largest: tile-local
-labelling + border merge, csrc/ipp_ccl.hip); the host reads back four ints per
+is left).  All work runs in libipp.so (ipp_ccl_keep_largest: bit-plane run
+labelling per 64×64 tile + border merge, csrc/ipp_ccl.hip); the host reads back four ints per
 image for the crop window.
 """
 from __future__ import annotations
@@ -33,7 +33,7 @@ class CclScratch:
             size = lib.ipp_ccl_scratch_layout(int(w), int(h), N.np_ptr(one))
             if size < 0:
                 N.check(int(size), "ipp_ccl_scratch_layout")
-            for f in ("lab_off", "p_off", "a_off", "ent_off", "tile_off"):
+            for f in (f for f in N.CCL_WORK.names if f.endswith("_off")):
                 self.works[i][f] = one[0][f] + base
             self.works[i]["ent_cap"] = one[0]["ent_cap"]
             self.max_ent = max(self.max_ent, int(one[0]["ent_cap"]))

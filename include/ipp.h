@@ -259,13 +259,15 @@ int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
 /* ------------------------------------------------------------------------ */
 /* Scratch of one image inside a caller-provided byte buffer (offsets in
  * bytes, 256-B aligned; ipp_ccl_scratch_layout fills them for a w×h image
- * relative to 0 — add the image's base offset).  lab: uint16 per pixel (local
- * root in its 64×32 tile); P/A: int32/uint32 per block-raster index (touched
- * at component roots only); ent: ent_cap {root, area, bbox} records. */
+ * relative to 0 — add the image's base offset).  Per 64×64 tile: mask = 64
+ * row words of fg bits (tile-major), edge = the global root of each edge
+ * pixel (top, bottom, left, right × 64 int32), tile = (first entry, count).
+ * P/A: int32/uint32 per run-start index (touched at component roots only);
+ * ent: ent_cap {root, area, bbox} records. */
 typedef struct ipp_ccl_work {
-    int64_t lab_off, p_off, a_off, ent_off;
+    int64_t mask_off, edge_off, p_off, a_off, ent_off;
     int64_t ent_cap;
-    int64_t tile_off;   /* per 64×32 tile: (first entry, entry count) */
+    int64_t tile_off;
 } ipp_ccl_work;
 
 /* Bytes of scratch for one w×h image; fills *work (may be NULL). */

@@ -312,6 +312,74 @@ def test_keep_largest_component_vs_oracle(D):
         assert np.array_equal(got, exp), im.shape
 
 
+def _ccl_stress_masks(rng):
+    """Foreground patterns for the bit-plane run labelling (64×64 tiles, lane =
+    row): densities around the 8-connected percolation threshold, the maximum
+    component count per tile (isolated pixels on the even grid: 1024 per
+    tile, many LDS stats passes, mixed tiles in the emit), a serpentine that
+    crosses every tile border many times (deep union-find chains), full rows
+    (runs reaching column 63), equal-area components in different tiles (tie
+    rule across tiles), and sizes off the tile grid."""
+    out = []
+    for (h, w), dens in [((130, 200), 0.3), ((129, 193), 0.42), ((200, 131), 0.6), ((64, 64), 0.5),
+                         ((65, 127), 0.45)]:
+        out.append(rng.random((h, w)) < dens)
+    grid = np.zeros((128, 192), bool)
+    grid[::2, ::2] = True
+    grid[100, 101] = grid[101, 102] = True          # one 3-pixel component wins
+    out.append(grid)
+    snake = np.zeros((300, 260), bool)
+    for c in range(0, 260, 3):
+        snake[:, c] = True
+        snake[0 if (c // 3) % 2 else 299, c:c + 3] = True
+    snake[150, 1] = False                            # notch: still one component
+    out.append(snake)
+    full = np.zeros((70, 190), bool)
+    full[3:9, :] = True
+    full[40, 5:70] = True
+    out.append(full)
+    tie = np.zeros((140, 150), bool)
+    tie[70:72, 100:103] = True                       # area 6, later block
+    tie[5:7, 130:133] = True                         # area 6, first block: wins
+    out.append(tie)
+    for (h, w) in [(1, 1), (1, 77), (77, 1), (2, 65)]:
+        out.append(rng.random((h, w)) < 0.6)
+    return out
+
+
+def test_keep_largest_component_stress(D):
+    from image_processor_pipeline_amd import device_ccl
+    rng = np.random.default_rng(31)
+    for fg in _ccl_stress_masks(rng):
+        if not fg.any():
+            continue
+        h, w = fg.shape
+        im = rng.integers(0, 256, (h, w, 4), np.uint8)
+        im[..., 3] = np.where(fg, rng.integers(2, 256, (h, w)), rng.integers(0, 2, (h, w)))
+        got = device_ccl.keep_largest_component(_t(im)).cpu().numpy()
+        exp = ops.keep_largest_component(im)
+        assert np.array_equal(got, exp), (h, w)
+
+
+def test_video_chain_noise_frames_vs_oracle(D):
+    """Fused config-5 chain on frames whose HSV mask is dense noise (many
+    components per tile, mixed tiles in the crop) and off-grid sizes."""
+    from image_processor_pipeline_amd import geometry as G
+    from image_processor_pipeline_amd.video_chain import VideoChain
+    rng = np.random.default_rng(5)
+    for (h, w, dens) in [(257, 389, 0.45), (130, 200, 0.6), (64, 128, 0.3)]:
+        n = 2
+        keep = np.array([220, 140, 40], np.uint8)        # kept colour (blue-ish)
+        drop = np.array([24, 18, 30], np.uint8)          # excluded (dark)
+        fr = np.where((rng.random((n, h, w)) < dens)[..., None], keep, drop).astype(np.uint8)
+        chain = VideoChain(n, h, w, DEV)
+        chain.run(_t(fr))
+        res = chain.results()
+        for i in range(n):
+            exp = ops.keep_largest_component(ops.color_mask_bgra(fr[i], G.REFERENCE_HSV_RANGES))
+            assert res[i] is not None and np.array_equal(res[i], exp), (h, w, i)
+
+
 # --------------------------------------------------------------------------- config 5: 4K video chain
 
 def test_video_chain_4k_vs_oracle(D):
