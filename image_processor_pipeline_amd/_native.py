@@ -71,7 +71,7 @@ HSV_PARAMS = np.dtype([("n_ranges", _I4), ("bgr", _I4), ("r", HSV_RANGE, (IPP_MA
 IMAGE_DESC = np.dtype([("off", _I8), ("w", _I4), ("h", _I4), ("pitch", _I4), ("cn", _I4)], align=True)
 
 CCL_WORK = np.dtype([("mask_off", _I8), ("edge_off", _I8), ("p_off", _I8), ("a_off", _I8), ("ent_off", _I8), ("ent_cap", _I8),
-                     ("tile_off", _I8)], align=True)
+                     ("tile_off", _I8), ("img_off", _I8)], align=True)
 
 RESAMPLE_DESC = np.dtype([
     ("src_off", _I8), ("dst_off", _I8), ("src_pitch", _I4), ("dst_pitch", _I4),

@@ -27,27 +27,29 @@
 //                    slots, with the runs of row r-1 it touches (8-adjacency:
 //                    columns a-1 .. b+1).  Compact component ids by a wave
 //                    scan; area / row and column masks per component by LDS
-//                    atomics in passes of MAXC ids; one entry per component
-//                    {global root G, area, bbox}; P[G] = G.  Written per
-//                    tile: the 64 mask words (tile-major), the global root of
-//                    every edge pixel (top, bottom, left, right; -1 for
-//                    background), (first entry, count).  No per-pixel label
-//                    plane: 1 bit per pixel plus 1 KB per tile.
-//   K2 k_ccl_border  unites the roots of 8-adjacent fg pixel pairs straddling
-//                    a tile border (edge arrays), skipping pairs a neighbouring
-//                    border pixel already unites (global atomicMin union-find
-//                    on P, touched only at roots).
-//   K3 k_ccl_resolve per entry: R = find(P, G); A[R] += area; P[G] = R.
-//   K4 k_ccl_best    per global root: atomicMax of (area << 32 | ~root).
-//   K5 k_ccl_bbox    per entry of the best component: bbox atomics.
-//   K6 k_ccl_emit    per tile meeting the output: which of its components are
-//                    in the best one (entries); a tile whose components are
-//                    all in (or all out) takes its mask words (or nothing); a
-//                    mixed tile relabels its mask words (the same
-//                    deterministic labelling as K1, so the same ids).  Then
-//                    α := 0 outside the component in place (plugin path), or
-//                    the crop-fit written as BGRA from the BGR frame (fused
-//                    chain).
+//                    atomics in passes of MAXC ids.  A component touching a
+//                    tile edge ("open") gets an entry {root G, area, bbox};
+//                    one that does not ("closed") is final here and competes
+//                    for the image's closed key by one 64-bit atomicMax.
+//                    Written per non-empty tile: the 64 mask words, the root
+//                    of every edge pixel, a record {components, the only
+//                    root, edge flags}.  No per-pixel label plane.
+//   K2 k_ccl_border  one wave per tile: unites the roots of 8-adjacent fg
+//                    pixel pairs across its right and bottom borders and its
+//                    two lower-right corners (only where both edge flags are
+//                    set), skipping pairs a neighbouring border pixel already
+//                    unites (global atomicMin union-find on P, at roots).
+//   K3 k_ccl_resolve per open entry: R = find(P, G); A[R] += area; P[G] = R.
+//   K4 k_ccl_best    per open root: atomicMax of (area << 32 | ~root).
+//   K5 k_ccl_bbox    the kept component = the better of the open and closed
+//                    bests; bbox from the closed key, or from its entries.
+//   K6 k_ccl_apply / k_ccl_crop_bgr, one wave per tile meeting the output:
+//                    a one-component tile takes its mask words or nothing; a
+//                    tile with several relabels its words (the same
+//                    deterministic labelling as K1, so the same ids) and looks
+//                    up each component's final root.  Then α := 0 outside the
+//                    component in place (plugin path), or the crop-fit written
+//                    as BGRA from the BGR frame (fused chain).
 // Pixels are read once in K1 and once in K6 (within the crop for the fused
 // chain); everything else is per run, per component or per edge pixel.
 #include <algorithm>
@@ -239,15 +241,30 @@ __device__ __forceinline__ int run_cid(const int* par, int j) {
 }
 
 // Scratch layout per image (offsets in the ipp_ccl_work descriptor).
+struct ImgRec {               // per-image record (img_off), zeroed by k_ccl_prep
+    u64 ckey;                 // best closed component (closed_key)
+    int32_t root;             // the kept component's root G, or -1 (k_ccl_bbox)
+    int32_t pad;
+};
+
+struct TileRec {              // per tile
+    int32_t n;                // components in the tile
+    int32_t g1;               // root G of the only component when n == 1
+    int32_t flags;            // fg on the tile's top / bottom / left / right edge
+    int32_t pad;
+};
+enum { F_TOP = 1, F_BOT = 2, F_LEFT = 4, F_RIGHT = 8 };
+
 struct Work {
     u64* mask;        // per tile 64 row words (tile-major)
     int32_t* edge;    // per tile 4 × 64 edge roots: top, bottom, left, right
     int32_t* P;       // 2*wb*hb parent array (touched at run-start roots only)
-    uint32_t* A;      // 2*wb*hb areas (touched at roots only)
-    int32_t* entL;    // per local component: global root index
+    uint32_t* A;      // 2*wb*hb areas (touched at open roots only)
+    int32_t* entL;    // per OPEN component: global root index
     uint32_t* entA;   // ... its in-tile area
     int4* entB;       // ... its bbox (x0, y0, x1, y1), image coordinates
-    int2* tile;       // per tile: (first entry, entry count)
+    TileRec* tile;
+    ImgRec* rec;
 };
 
 __device__ __forceinline__ Work work_of(uint8_t* scratch, const ipp_ccl_work& w) {
@@ -259,11 +276,24 @@ __device__ __forceinline__ Work work_of(uint8_t* scratch, const ipp_ccl_work& w)
     k.entL = reinterpret_cast<int32_t*>(scratch + w.ent_off);
     k.entA = reinterpret_cast<uint32_t*>(scratch + w.ent_off) + w.ent_cap;
     k.entB = reinterpret_cast<int4*>(scratch + w.ent_off + 8 * w.ent_cap);
-    k.tile = reinterpret_cast<int2*>(scratch + w.tile_off);
+    k.tile = reinterpret_cast<TileRec*>(scratch + w.tile_off);
+    k.rec = reinterpret_cast<ImgRec*>(scratch + w.img_off);
     return k;
 }
 
 enum { E_TOP = 0, E_BOT = 1, E_LEFT = 2, E_RIGHT = 3 };
+
+// Closed components (no pixel on a tile edge) are final after K1: they never
+// take part in a union.  Their best is kept per image in one 64-bit key whose
+// order is the selection order (area, then smaller root):
+//   area (13 bits) << 51 | (~G & 0x7FFFFF) << 24 | in-tile bbox (4 × 6 bits).
+// Images with 2·wb·hb > 2^23 run-start slots treat every component as open.
+constexpr int64_t CLOSED_SLOTS = 1 << 23;
+
+__device__ __forceinline__ u64 closed_key(uint32_t area, int32_t G, int bx0, int by0, int bx1, int by1) {
+    return ((u64)area << 51) | ((u64)(~(uint32_t)G & 0x7FFFFFu) << 24) |
+           (u64)(bx0 | (by0 << 6) | ((bx1 - 1) << 12) | ((by1 - 1) << 18));
+}
 
 // Foreground source: α > 1 of a 4-channel image, or the HSV mask of a
 // 3-channel BGR image (fused chain).
@@ -348,6 +378,7 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
     __shared__ int par_s[WAVES][NJ];
     __shared__ uint32_t st_area[WAVES][MAXC];
     __shared__ u64 st_rows[WAVES][MAXC], st_cols[WAVES][MAXC];
+    __shared__ int st_root[WAVES][MAXC];
     struct NoTables {};
     __shared__ typename std::conditional<SRC == SRC_HSV, HsvTables<NR>, NoTables>::type T;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
@@ -368,42 +399,46 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
     if (tx >= f.tiles_x || ty >= f.tiles_y) return;  // wave-uniform; no barrier follows
     int* par = par_s[wave];
     const Work k = work_of(scratch, works[im]);
-    const int x = tx * TW + lane, y0 = ty * TH;
+    const int x = tx * TW + lane, y0 = ty * TH, X0 = tx * TW;
+    const int tile = ty * f.tiles_x + tx;
 
     // A. mask words.
     u64 m, p;
     const HsvTables<NR>* Tp = nullptr;
     if constexpr (SRC == SRC_HSV) Tp = &T;
-    if (tx * TW + TW <= d.w && y0 + TH < d.h)
+    if (X0 + TW <= d.w && y0 + TH < d.h)
         tile_words<SRC, NR, ZONES, true>(img, d, x, y0, lane, Tp, R, m, p);
     else
         tile_words<SRC, NR, ZONES, false>(img, d, x, y0, lane, Tp, R, m, p);
-    k.mask[(int64_t)(ty * f.tiles_x + tx) * TH + lane] = m;
+    if (__ballot(m != 0ull) == 0ull) {  // no foreground: K2 and K6 skip the tile by its record
+        if (lane == 0) k.tile[tile] = TileRec{0, -1, 0, 0};
+        return;
+    }
+    k.mask[(int64_t)tile * TH + lane] = m;
 
     // B-F. runs, unions, component ids.
     const int r = lane;
     const int n = label_tile(par, r, lane, m, p);
-    int base = 0;
-    if (lane == 0 && n > 0) base = atomicAdd(&counts[im], n);
-    base = __shfl(base, 0);
-    if (lane == 0) k.tile[ty * f.tiles_x + tx] = make_int2(base, n);
+    const bool closed_ok = 2ll * f.wb * ((f.h + 1) >> 1) <= CLOSED_SLOTS;
 
-    // Entries: roots write the global root; P / A initialised there.
+    // P[G] = G at every root (the emit reads P for closed roots too).
+    int32_t g1 = -1;
     for_runs(m, [&](int a, int) {
         const int j = slot(r, a);
-        const int v = par[j];
-        if (v >= NJ) {
+        if (par[j] >= NJ) {
             const int32_t G = slot_gidx(f, tx, ty, j);
-            k.entL[base + v - NJ] = G;
             k.P[G] = G;
-            k.A[G] = 0u;
+            g1 = G;
         }
     });
 
-    // Stats per component, MAXC ids per pass.
+    // Stats per component, MAXC ids per pass; open components get entries,
+    // closed ones compete for the image's closed key.
     uint32_t* area = st_area[wave];
     u64* rows = st_rows[wave];
     u64* cols = st_cols[wave];
+    int* croot = st_root[wave];
+    u64 best_closed = 0ull;
     for (int c0 = 0; c0 < n; c0 += MAXC) {
         if (lane < MAXC) {
             area[lane] = 0u;
@@ -412,108 +447,126 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
         }
         wave_sync();
         for_runs(m, [&](int a, int len) {
-            const int c = run_cid(par, slot(r, a)) - c0;
+            const int j = slot(r, a);
+            const int v = par[j];
+            const int c = (v >= NJ ? v : par[v]) - NJ - c0;
             if ((unsigned)c < (unsigned)MAXC) {
                 atomicAdd(&area[c], (uint32_t)len);
                 atomicOr(&rows[c], 1ull << r);
                 atomicOr(&cols[c], run_mask(a, len));
+                if (v >= NJ) croot[c] = j;
             }
         });
         wave_sync();
-        if (lane < MAXC && c0 + lane < n) {
-            const int e = base + c0 + lane;
-            const u64 cm = cols[lane], rm = rows[lane];
-            const int X0 = tx * TW;
-            k.entA[e] = area[lane];
-            k.entB[e] = make_int4(X0 + ctz64(cm), y0 + ctz64(rm), X0 + 64 - __clzll(cm), y0 + 64 - __clzll(rm));
+        const bool valid = lane < MAXC && c0 + lane < n;
+        u64 cm = 0ull, rm = 0ull;
+        uint32_t ar = 0u;
+        int32_t G = 0;
+        if (valid) {
+            cm = cols[lane];
+            rm = rows[lane];
+            ar = area[lane];
+            G = slot_gidx(f, tx, ty, croot[lane]);
+        }
+        const bool edge = ((cm | rm) & (1ull | (1ull << 63))) != 0ull;
+        const bool open = valid && (edge || !closed_ok);
+        const int bx0 = ctz64(cm), by0 = ctz64(rm), bx1 = 64 - __clzll(cm), by1 = 64 - __clzll(rm);
+        if (valid && !open) {
+            const u64 key = closed_key(ar, G, bx0, by0, bx1, by1);
+            best_closed = key > best_closed ? key : best_closed;
+        }
+        const u64 om = __ballot(open);
+        if (om) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&counts[im], __popcll(om));
+            base = __shfl(base, 0);
+            if (open) {
+                const int e = base + __popcll(om & ((1ull << lane) - 1ull));
+                k.entL[e] = G;
+                k.entA[e] = ar;
+                k.entB[e] = make_int4(X0 + bx0, y0 + by0, X0 + bx1, y0 + by1);
+                k.A[G] = 0u;
+            }
         }
         wave_sync();
     }
-
-    // Edge roots (global G of the pixel's root, -1 for background).
-    int32_t* edge = k.edge + (int64_t)(ty * f.tiles_x + tx) * (4 * 64);
-    {
-        const u64 s = m & ~(m << 1);
-        // left / right: lane r's own row
-        edge[E_LEFT * 64 + lane] = (m & 1ull) ? slot_gidx(f, tx, ty, run_root(par, slot(r, 0))) : -1;
-        edge[E_RIGHT * 64 + lane] =
-            (m >> 63) ? slot_gidx(f, tx, ty, run_root(par, slot(r, 63 - __clzll(s)))) : -1;
-        // top / bottom: lane = column of rows 0 and 63
-        const u64 m0 = __shfl(m, 0), m63 = __shfl(m, TH - 1);
-        const u64 upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-        int32_t t = -1, bo = -1;
-        if ((m0 >> lane) & 1ull) {
-            const u64 s0 = m0 & ~(m0 << 1) & upto;
-            t = slot_gidx(f, tx, ty, run_root(par, slot(0, 63 - __clzll(s0))));
-        }
-        if ((m63 >> lane) & 1ull) {
-            const u64 s63 = m63 & ~(m63 << 1) & upto;
-            bo = slot_gidx(f, tx, ty, run_root(par, slot(TH - 1, 63 - __clzll(s63))));
-        }
-        edge[E_TOP * 64 + lane] = t;
-        edge[E_BOT * 64 + lane] = bo;
+    for (int off = 32; off > 0; off >>= 1) {
+        const u64 o = __shfl_xor(best_closed, off);
+        best_closed = o > best_closed ? o : best_closed;
     }
+    if (lane == 0 && best_closed) atomicMax(&k.rec[0].ckey, best_closed);
+
+    // Edge roots (global G of the pixel's root, -1 for background) and flags.
+    int32_t* edge = k.edge + (int64_t)tile * (4 * 64);
+    const u64 s = m & ~(m << 1);
+    edge[E_LEFT * 64 + lane] = (m & 1ull) ? slot_gidx(f, tx, ty, run_root(par, slot(r, 0))) : -1;
+    edge[E_RIGHT * 64 + lane] = (m >> 63) ? slot_gidx(f, tx, ty, run_root(par, slot(r, 63 - __clzll(s)))) : -1;
+    const u64 m0 = __shfl(m, 0), m63 = __shfl(m, TH - 1);
+    const u64 upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    int32_t t = -1, bo = -1;
+    if ((m0 >> lane) & 1ull) t = slot_gidx(f, tx, ty, run_root(par, slot(0, 63 - __clzll(m0 & ~(m0 << 1) & upto))));
+    if ((m63 >> lane) & 1ull)
+        bo = slot_gidx(f, tx, ty, run_root(par, slot(TH - 1, 63 - __clzll(m63 & ~(m63 << 1) & upto))));
+    edge[E_TOP * 64 + lane] = t;
+    edge[E_BOT * 64 + lane] = bo;
+    const u64 lb = __ballot(m & 1ull), rbits = __ballot(m >> 63);
+    g1 = __shfl(g1, 63 - (int)__clzll(__ballot(g1 >= 0) | 1ull));
+    if (lane == 0)
+        k.tile[tile] = TileRec{n, n == 1 ? g1 : -1,
+                               (m0 ? F_TOP : 0) | (m63 ? F_BOT : 0) | (lb ? F_LEFT : 0) | (rbits ? F_RIGHT : 0), 0};
 }
 
-// Root of pixel (x, y) on a tile edge, from that tile's edge array.
-__device__ __forceinline__ int32_t edge_root(const Frame& f, const Work& k, int x, int y, int which) {
-    const int tx = x / TW, ty = y / TH;
-    const int i = (which == E_LEFT || which == E_RIGHT) ? (y - ty * TH) : (x - tx * TW);
-    return k.edge[(int64_t)(ty * f.tiles_x + tx) * (4 * 64) + which * 64 + i];
+// K2: one wave per tile T unites across its right border (pairs with the
+// tile to the right, rows of one tile row), its bottom border, and the two
+// corner pairs below-right: (63, 63)@T – (0, 0)@T+x+y and (0, 63)@T+x –
+// (63, 0)@T+y.  Along a border, consecutive pixels usually see the same pair
+// of roots: a pair is skipped when the previous (next) pixel with the same
+// near-side root takes it, so a long shared boundary costs one union.
+__device__ __forceinline__ void border_pairs(int32_t* P, const int32_t* near, const int32_t* far, int lane) {
+    const int32_t a = near[lane];
+    if (a < 0) return;
+    const int32_t ap = lane > 0 ? near[lane - 1] : -1, an = lane < 63 ? near[lane + 1] : -1;
+    const int32_t cp = lane > 0 ? far[lane - 1] : -1, c0 = far[lane], cn = lane < 63 ? far[lane + 1] : -1;
+    if (cp >= 0 && ap != a) gunite(P, a, cp);
+    if (c0 >= 0 && !(ap == a && cp == c0)) gunite(P, a, c0);
+    if (cn >= 0 && an != a) gunite(P, a, cn);
 }
 
-// Border pairs.  Thread i < vert owns left pixel (64*bx - 1, y) of a vertical
-// tile border and its 8-neighbours (64*bx, y-1..y+1); the rest own the upper
-// pixel (x, 64*by - 1) of a horizontal border and (x-1..x+1, 64*by).  Along a
-// border, consecutive owners usually see the same pair of roots: a pair is
-// skipped when the previous (next) owner with the same near-side root takes
-// it, so a long shared boundary costs one union, not one per pixel.
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(64 * WAVES)
 k_ccl_border(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
-             uint8_t* __restrict__ scratch, int chunks) {
+             uint8_t* __restrict__ scratch, int groups_per_img, int groups_x) {
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / chunks;
-    const int64_t i = (int64_t)(b - (uint32_t)im * chunks) * 256 + threadIdx.x;
+    const int im = b / groups_per_img;
+    const int g = b - im * groups_per_img;
+    const int ty = g / groups_x;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int tx = (g - ty * groups_x) * WAVES + wave;
     const ipp_image_desc d = descs[im];
     const Frame f = frame_of(d);
+    if (tx >= f.tiles_x || ty >= f.tiles_y) return;
     const Work k = work_of(scratch, works[im]);
-    const int64_t vert = (int64_t)(f.tiles_x - 1) * f.h;
-    const int64_t horz = (int64_t)(f.tiles_y - 1) * f.w;
-    int nx, ny, sx, sy, fx, fy, pos, len, near_e, far_e;
-    if (i < vert) {
-        const int bx = 1 + (int)(i / f.h);
-        pos = (int)(i % f.h);
-        len = f.h;
-        nx = bx * TW - 1, ny = pos, sx = 0, sy = 1, fx = 1, fy = 0;
-        near_e = E_RIGHT, far_e = E_LEFT;
-    } else if (i < vert + horz) {
-        const int64_t j = i - vert;
-        const int by = 1 + (int)(j / f.w);
-        pos = (int)(j % f.w);
-        len = f.w;
-        nx = pos, ny = by * TH - 1, sx = 1, sy = 0, fx = 0, fy = 1;
-        near_e = E_BOT, far_e = E_TOP;
-    } else {
-        return;
+    const int tile = ty * f.tiles_x + tx;
+    const bool has_r = tx + 1 < f.tiles_x, has_b = ty + 1 < f.tiles_y;
+    const int fl = k.tile[tile].flags;
+    const int fr = has_r ? k.tile[tile + 1].flags : 0;
+    const int fb = has_b ? k.tile[tile + f.tiles_x].flags : 0;
+    auto E = [&](int t, int which) { return k.edge + (int64_t)t * (4 * 64) + which * 64; };
+    if ((fl & F_RIGHT) && (fr & F_LEFT)) border_pairs(k.P, E(tile, E_RIGHT), E(tile + 1, E_LEFT), lane);
+    if ((fl & F_BOT) && (fb & F_TOP)) border_pairs(k.P, E(tile, E_BOT), E(tile + f.tiles_x, E_TOP), lane);
+    if (lane == 0 && has_r && has_b) {
+        const int32_t a = (fl & F_BOT) ? E(tile, E_BOT)[63] : -1;
+        const int32_t c = (k.tile[tile + f.tiles_x + 1].flags & F_TOP) ? E(tile + f.tiles_x + 1, E_TOP)[0] : -1;
+        if (a >= 0 && c >= 0) gunite(k.P, a, c);
+        const int32_t a2 = (fr & F_BOT) ? E(tile + 1, E_BOT)[0] : -1;
+        const int32_t c2 = (fb & F_TOP) ? E(tile + f.tiles_x, E_TOP)[63] : -1;
+        if (a2 >= 0 && c2 >= 0) gunite(k.P, a2, c2);
     }
-    const int32_t a = edge_root(f, k, nx, ny, near_e);
-    if (a < 0) return;
-    auto near_at = [&](int q) {
-        return (q < 0 || q >= len) ? -1 : edge_root(f, k, nx + (q - pos) * sx, ny + (q - pos) * sy, near_e);
-    };
-    auto far_at = [&](int q) {
-        return (q < 0 || q >= len) ? -1 : edge_root(f, k, nx + fx + (q - pos) * sx, ny + fy + (q - pos) * sy, far_e);
-    };
-    const int32_t ap = near_at(pos - 1), an = near_at(pos + 1);
-    const int32_t cp = far_at(pos - 1), c0 = far_at(pos), cn = far_at(pos + 1);
-    if (cp >= 0 && ap != a) gunite(k.P, a, cp);
-    if (c0 >= 0 && !(ap == a && cp == c0)) gunite(k.P, a, c0);
-    if (cn >= 0 && an != a) gunite(k.P, a, cn);
 }
 
-// Entry kernels run ENT_BLOCKS blocks per image striding over the image's
-// entry count (known only on the device).
-constexpr int ENT_BLOCKS = 32;
+// Entry kernels (open components only) run ENT_BLOCKS blocks per image
+// striding over the image's entry count (known only on the device).
+constexpr int ENT_BLOCKS = 16;
 
 __global__ void __launch_bounds__(256)
 k_ccl_resolve(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch,
@@ -553,26 +606,44 @@ k_ccl_best(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch
     if ((threadIdx.x & 63) == 0 && key) atomicMax(best + im, key);
 }
 
-__device__ __forceinline__ int32_t best_root(unsigned long long key) {
-    return key ? (int32_t)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull)) : -1;
-}
-
-// K5: bbox of the best component = union of its entries' tile bboxes.
+// K5: the kept component = the larger of the best open one (best[im]: area
+// << 32 | ~root) and the best closed one (rec.ckey), the smaller root on equal
+// areas; its bbox = the closed key's tile bbox, or the union of its open
+// entries' tile bboxes.  The image's first block records the root for K6.
 __global__ void __launch_bounds__(256)
-k_ccl_bbox(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, const int32_t* __restrict__ counts,
+k_ccl_bbox(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
+           uint8_t* __restrict__ scratch, const int32_t* __restrict__ counts,
            const unsigned long long* __restrict__ best, int32_t* __restrict__ bbox) {
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int im = b / ENT_BLOCKS;
-    const int32_t broot = best_root(best[im]);
+    const int blk = b - im * ENT_BLOCKS;
+    const Work k = work_of(scratch, works[im]);
+    const u64 ko = best[im], kc = k.rec->ckey;
+    const uint32_t ao = (uint32_t)(ko >> 32), ac = (uint32_t)(kc >> 51);
+    const int32_t go = ko ? (int32_t)(0xFFFFFFFFu - (uint32_t)ko) : -1;
+    const int32_t gc = kc ? (int32_t)(~(uint32_t)(kc >> 24) & 0x7FFFFFu) : -1;
+    const bool closed_wins = kc && (!ko || ac > ao || (ac == ao && gc < go));
+    const int32_t broot = closed_wins ? gc : go;
+    if (blk == 0 && threadIdx.x == 0) {
+        k.rec->root = broot;
+        if (closed_wins) {
+            const Frame f = frame_of(descs[im]);
+            const int yb = (gc >> 1) / f.wb;
+            const int tx = ((gc >> 1) - yb * f.wb) / (TW / 2), ty = (2 * yb + (gc & 1)) / TH;
+            const uint32_t q = (uint32_t)(kc & 0xFFFFFFu);
+            bbox[4 * im + 0] = tx * TW + (int)(q & 63u);
+            bbox[4 * im + 1] = ty * TH + (int)((q >> 6) & 63u);
+            bbox[4 * im + 2] = tx * TW + (int)((q >> 12) & 63u) + 1;
+            bbox[4 * im + 3] = ty * TH + (int)((q >> 18) & 63u) + 1;
+        }
+    }
+    if (closed_wins || broot < 0) return;
     int4 bb = make_int4(INT32_MAX, INT32_MAX, -1, -1);
-    if (broot >= 0) {
-        const int n = counts[im];
-        const Work k = work_of(scratch, works[im]);
-        for (int e = (int)(b - (uint32_t)im * ENT_BLOCKS) * 256 + threadIdx.x; e < n; e += ENT_BLOCKS * 256) {
-            if (k.P[k.entL[e]] == broot) {
-                const int4 q = k.entB[e];
-                bb = make_int4(min(bb.x, q.x), min(bb.y, q.y), max(bb.z, q.z), max(bb.w, q.w));
-            }
+    const int n = counts[im];
+    for (int e = blk * 256 + threadIdx.x; e < n; e += ENT_BLOCKS * 256) {
+        if (k.P[k.entL[e]] == broot) {
+            const int4 q = k.entB[e];
+            bb = make_int4(min(bb.x, q.x), min(bb.y, q.y), max(bb.z, q.z), max(bb.w, q.w));
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -589,119 +660,129 @@ k_ccl_bbox(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch
     }
 }
 
-// K6 front half (one block per tile): the tile's row words restricted to
-// the best component, into inw[64].  Every thread of the block takes part.
-struct EmitLds {
-    u64 inw[TH];
-    uint8_t flag[CMAX];
-    int par[NJ];
-    int any;  // bit 0: a component in the best one, bit 1: one outside it
-};
-
-__device__ __forceinline__ void tile_in_words(const Frame& f, const Work& k, int tx, int ty, int32_t broot,
-                                              EmitLds& L) {
-    const int tile = ty * f.tiles_x + tx;
-    const int2 te = k.tile[tile];
-    if (threadIdx.x == 0) L.any = 0;
-    __syncthreads();
-    int any = 0;
-    for (int e = threadIdx.x; e < te.y; e += blockDim.x) {
-        const bool in = k.P[k.entL[te.x + e]] == broot;
-        L.flag[e] = in ? 1 : 0;
-        any |= in ? 1 : 2;
-    }
-    if (any) atomicOr(&L.any, any);
-    __syncthreads();
-    const int mode = L.any;
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        const u64 m = k.mask[(int64_t)tile * TH + lane];
-        u64 w = 0ull;
-        if (mode == 1) {
-            w = m;
-        } else if (mode == 3) {
-            const u64 p = __shfl_up(m, 1);
-            label_tile(L.par, lane, lane, m, lane > 0 ? p : 0ull);
-            for_runs(m, [&](int a, int len) {
-                if (L.flag[run_cid(L.par, slot(lane, a))]) w |= run_mask(a, len);
-            });
-        }
-        L.inw[lane] = w;
-    }
-    __syncthreads();
+// K6 front half, one wave per tile: the tile's row words restricted to the
+// kept component (lane r: row r).  A tile with one component takes its mask
+// words or nothing; a tile with several relabels its words (same ids as K1)
+// and looks up each component's final root.
+__device__ __forceinline__ u64 tile_in_word(const Frame& f, const Work& k, int tile, int32_t broot, int lane,
+                                            int* par, uint8_t* cflag, int tx, int ty) {
+    const TileRec t = k.tile[tile];
+    if (t.n == 0) return 0ull;
+    const u64 m = k.mask[(int64_t)tile * TH + lane];
+    if (t.n == 1) return k.P[t.g1] == broot ? m : 0ull;
+    const u64 p = __shfl_up(m, 1);
+    label_tile(par, lane, lane, m, lane > 0 ? p : 0ull);
+    for_runs(m, [&](int a, int) {
+        const int j = slot(lane, a);
+        const int v = par[j];
+        if (v >= NJ) cflag[v - NJ] = k.P[slot_gidx(f, tx, ty, j)] == broot;
+    });
+    wave_sync();
+    u64 w = 0ull;
+    for_runs(m, [&](int a, int len) {
+        if (cflag[run_cid(par, slot(lane, a))]) w |= run_mask(a, len);
+    });
+    return w;
 }
 
-// K6, plugin path: in place on a 4-channel image, α := 0 outside the best
+__device__ __forceinline__ u64 row_word(u64 w, int r) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)w, r);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(w >> 32), r);
+    return ((u64)hi << 32) | lo;
+}
+
+// K6, plugin path: in place on a 4-channel image, α := 0 outside the kept
 // component (images without any component are left unchanged).
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(64 * WAVES)
 k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
-            uint8_t* __restrict__ scratch, const unsigned long long* __restrict__ best, int tiles_per_img,
-            int tiles_x_max) {
-    __shared__ EmitLds L;
+            uint8_t* __restrict__ scratch, int groups_per_img, int groups_x) {
+    __shared__ int par_s[WAVES][NJ];
+    __shared__ uint8_t flag_s[WAVES][CMAX];
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / tiles_per_img;
-    const int t = b - im * tiles_per_img;
-    const int ty = t / tiles_x_max, tx = t - ty * tiles_x_max;
+    const int im = b / groups_per_img;
+    const int g = b - im * groups_per_img;
+    const int ty = g / groups_x;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int tx = (g - ty * groups_x) * WAVES + wave;
     const ipp_image_desc d = descs[im];
     const Frame f = frame_of(d);
     if (tx >= f.tiles_x || ty >= f.tiles_y) return;
-    const int32_t broot = best_root(best[im]);
-    if (broot < 0) return;
     const Work k = work_of(scratch, works[im]);
-    tile_in_words(f, k, tx, ty, broot, L);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int32_t broot = k.rec->root;
+    if (broot < 0) return;
+    const u64 w = tile_in_word(f, k, ty * f.tiles_x + tx, broot, lane, par_s[wave], flag_s[wave], tx, ty);
     const int x = tx * TW + lane;
-    if (x >= d.w) return;
-    for (int r = wave; r < TH; r += 4) {
-        const int y = ty * TH + r;
-        if (y >= d.h) break;
-        if (!((L.inw[r] >> lane) & 1ull)) {
-            uint8_t* a = img + d.off + (int64_t)y * d.pitch + 4 * (int64_t)x + 3;
+    const int nr = min(TH, d.h - ty * TH);
+    for (int r = 0; r < nr; ++r) {
+        const u64 rw = row_word(w, r);
+        if (x < d.w && !((rw >> lane) & 1ull)) {
+            uint8_t* a = img + d.off + (int64_t)(ty * TH + r) * d.pitch + 4 * (int64_t)x + 3;
             if (*a) *a = 0;
         }
     }
 }
 
-// K6, fused chain: crop-fit of the BGR frame to the best component's bbox,
+// K6, fused chain: crop-fit of the BGR frame to the kept component's bbox,
 // written as BGRA (α = 255 inside the component, 0 elsewhere) into the image's
-// output slot; one block per labelling tile that meets the bbox.
-__global__ void __launch_bounds__(256)
+// output slot; one wave per tile that meets the bbox.  The first rows' pixel
+// loads are issued before the tile's words are worked out.
+__global__ void __launch_bounds__(64 * WAVES)
 k_ccl_crop_bgr(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
                const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch,
-               const unsigned long long* __restrict__ best, const int32_t* __restrict__ bbox,
-               uint8_t* __restrict__ out, const ipp_image_desc* __restrict__ out_descs, int tiles_per_img,
-               int tiles_x_max) {
-    __shared__ EmitLds L;
+               const int32_t* __restrict__ bbox, uint8_t* __restrict__ out,
+               const ipp_image_desc* __restrict__ out_descs, int groups_per_img, int groups_x) {
+    __shared__ int par_s[WAVES][NJ];
+    __shared__ uint8_t flag_s[WAVES][CMAX];
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / tiles_per_img;
-    const int t = b - im * tiles_per_img;
-    const int ty = t / tiles_x_max, tx = t - ty * tiles_x_max;
+    const int im = b / groups_per_img;
+    const int g = b - im * groups_per_img;
+    const int ty = g / groups_x;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int tx = (g - ty * groups_x) * WAVES + wave;
     const ipp_image_desc d = descs[im];
     const Frame f = frame_of(d);
     if (tx >= f.tiles_x || ty >= f.tiles_y) return;
-    const int32_t broot = best_root(best[im]);
+    const Work k = work_of(scratch, works[im]);
+    const int32_t broot = k.rec->root;
     if (broot < 0) return;
     const int bx0 = bbox[4 * im + 0], by0 = bbox[4 * im + 1], bx1 = bbox[4 * im + 2], by1 = bbox[4 * im + 3];
-    if (tx * TW >= bx1 || (tx + 1) * TW <= bx0 || ty * TH >= by1 || (ty + 1) * TH <= by0) return;
-    const Work k = work_of(scratch, works[im]);
-    tile_in_words(f, k, tx, ty, broot, L);
+    const int X0 = tx * TW, Y0 = ty * TH;
+    if (X0 >= bx1 || X0 + TW <= bx0 || Y0 >= by1 || Y0 + TH <= by0) return;
+    const int r0 = max(0, by0 - Y0), r1 = min(TH, by1 - Y0);
+    const int x = X0 + lane;
+    const bool xin = x >= bx0 && x < bx1;
+    const uint8_t* src = img + d.off + (int64_t)Y0 * d.pitch + 3 * (int64_t)x;
+    const bool last_col = x == d.w - 1;
+    auto load = [&](int r) -> uint32_t {
+        if (!xin) return 0u;
+        const uint8_t* q = src + (int64_t)r * d.pitch;
+        return load_rgb_opaque(q, !last_col || Y0 + r < d.h - 1);
+    };
+    uint32_t px[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) px[i] = r0 + i < r1 ? load(r0 + i) : 0u;
+    const u64 w = tile_in_word(f, k, ty * f.tiles_x + tx, broot, lane, par_s[wave], flag_s[wave], tx, ty);
     const ipp_image_desc od = out_descs[im];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = tx * TW + lane;
-    if (x < bx0 || x >= bx1) return;
-    const int r0 = max(wave, by0 - ty * TH + ((wave - (by0 - ty * TH)) & 3));
-    for (int r = r0; r < TH; r += 4) {
-        const int y = ty * TH + r;
-        if (y >= by1) break;
-        const bool wide_ok = (y < d.h - 1) || (x < d.w - 1);
-        const uint32_t px = load_rgb_opaque(img + d.off + (int64_t)y * d.pitch + 3 * (int64_t)x, wide_ok);
-        const bool in = (L.inw[r] >> lane) & 1ull;
-        reinterpret_cast<uint32_t*>(out + od.off + (int64_t)(y - by0) * od.pitch)[x - bx0] =
-            (px & 0x00FFFFFFu) | (in ? 0xFF000000u : 0u);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(out + od.off) + (x - bx0);
+    for (int rb = r0; rb < r1; rb += RB) {
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+            const int r = rb + i;
+            if (r < r1) {
+                const u64 rw = row_word(w, r);
+                if (xin)
+                    *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(dst) + (int64_t)(Y0 + r - by0) * od.pitch) =
+                        (px[i] & 0x00FFFFFFu) | (((rw >> lane) & 1ull) ? 0xFF000000u : 0u);
+                px[i] = r + RB < r1 ? load(r + RB) : 0u;
+            }
+        }
     }
 }
 
-__global__ void k_ccl_prep(int32_t* bbox, unsigned long long* best, int32_t* counts, int n) {
+__global__ void k_ccl_prep(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, int32_t* bbox,
+                           unsigned long long* best, int32_t* counts, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
         bbox[4 * i + 0] = INT32_MAX;
@@ -710,6 +791,9 @@ __global__ void k_ccl_prep(int32_t* bbox, unsigned long long* best, int32_t* cou
         bbox[4 * i + 3] = -1;
         best[i] = 0ull;
         counts[i] = 0;
+        ImgRec* rec = reinterpret_cast<ImgRec*>(scratch + works[i].img_off);
+        rec->ckey = 0ull;
+        rec->root = -1;
     }
 }
 
@@ -719,9 +803,8 @@ __global__ void k_ccl_finish(int32_t* bbox, int n) {
 }
 
 struct Launch {
-    int tiles_x, tiles_y, tiles_per_img, groups_x, groups_per_img;
-    int border_chunks, ent_chunks;
-    dim3 tile_grid, group_grid, border_grid, ent_grid;
+    int tiles_x, tiles_y, groups_x, groups_per_img;
+    dim3 group_grid, ent_grid;
     bool ok;
 };
 
@@ -729,18 +812,11 @@ Launch plan_launch(int n, int max_w, int max_h) {
     Launch L{};
     L.tiles_x = (max_w + TW - 1) / TW;
     L.tiles_y = (max_h + TH - 1) / TH;
-    L.tiles_per_img = L.tiles_x * L.tiles_y;
     L.groups_x = (L.tiles_x + WAVES - 1) / WAVES;
     L.groups_per_img = L.groups_x * L.tiles_y;
-    const int64_t border = (int64_t)(L.tiles_x - 1) * max_h + (int64_t)(L.tiles_y - 1) * max_w;
-    L.border_chunks = (int)std::max<int64_t>(1, (border + 255) / 256);
-    L.ent_chunks = ENT_BLOCKS;
-    const int64_t tb = (int64_t)L.tiles_per_img * n, gb = (int64_t)L.groups_per_img * n,
-                  bb = (int64_t)L.border_chunks * n, eb = (int64_t)L.ent_chunks * n;
-    L.ok = tb < INT32_MAX && gb < INT32_MAX && bb < INT32_MAX && eb < INT32_MAX;
-    L.tile_grid = dim3((uint32_t)tb);
+    const int64_t gb = (int64_t)L.groups_per_img * n, eb = (int64_t)ENT_BLOCKS * n;
+    L.ok = gb < INT32_MAX && eb < INT32_MAX;
     L.group_grid = dim3((uint32_t)gb);
-    L.border_grid = dim3((uint32_t)bb);
     L.ent_grid = dim3((uint32_t)eb);
     return L;
 }
@@ -759,7 +835,7 @@ int run_labels(int src, const uint8_t* img, const ipp_image_desc* descs, int32_t
     L = plan_launch(n, max_w, max_h);
     if (!L.ok) return IPP_E_ARG;
     const int nb = (n + 255) / 256;
-    hipLaunchKernelGGL(k_ccl_prep, dim3(nb), dim3(256), 0, s, bbox, best, counts, n);
+    hipLaunchKernelGGL(k_ccl_prep, dim3(nb), dim3(256), 0, s, works, scratch, bbox, best, counts, n);
     if (src == SRC_ALPHA) {
         launch_label<SRC_ALPHA, 1, false>(L, s, img, descs, works, scratch, counts, ipp_hsv_params{});
     } else {
@@ -771,10 +847,11 @@ int run_labels(int src, const uint8_t* img, const ipp_image_desc* descs, int32_t
         else if (!zones) launch_label<SRC_HSV, IPP_MAX_HSV_RANGES, false>(L, s, img, descs, works, scratch, counts, q);
         else launch_label<SRC_HSV, IPP_MAX_HSV_RANGES, true>(L, s, img, descs, works, scratch, counts, q);
     }
-    hipLaunchKernelGGL(k_ccl_border, L.border_grid, dim3(256), 0, s, descs, works, scratch, L.border_chunks);
+    hipLaunchKernelGGL(k_ccl_border, L.group_grid, dim3(64 * WAVES), 0, s, descs, works, scratch, L.groups_per_img,
+                       L.groups_x);
     hipLaunchKernelGGL(k_ccl_resolve, L.ent_grid, dim3(256), 0, s, works, scratch, counts);
     hipLaunchKernelGGL(k_ccl_best, L.ent_grid, dim3(256), 0, s, works, scratch, counts, best);
-    hipLaunchKernelGGL(k_ccl_bbox, L.ent_grid, dim3(256), 0, s, works, scratch, counts, best, bbox);
+    hipLaunchKernelGGL(k_ccl_bbox, L.ent_grid, dim3(256), 0, s, descs, works, scratch, counts, best, bbox);
     return IPP_OK;
 }
 
@@ -786,17 +863,21 @@ extern "C" int64_t ipp_ccl_scratch_layout(int32_t w, int32_t h, ipp_ccl_work* wo
     const int64_t slots = 2 * wb * hb;
     if (slots >= INT32_MAX) return IPP_E_RANGE;
     const int64_t tiles = (int64_t)((w + TW - 1) / TW) * ((h + TH - 1) / TH);
-    const int64_t cap = tiles * CMAX;
+    // open components only when closed keys fit (see CLOSED_SLOTS): each
+    // touches the tile's ring of 252 edge pixels, and two of them are never
+    // adjacent on it (≤ 126 per tile); else every component (≤ CMAX per tile)
+    const int64_t cap = tiles * (slots <= CLOSED_SLOTS ? 128 : CMAX);
     auto al = [](int64_t v) { return (v + 255) & ~(int64_t)255; };
     ipp_ccl_work k{};
-    k.mask_off = 0;
-    k.edge_off = al(8 * TH * tiles);
+    k.img_off = 0;
+    k.mask_off = 256;
+    k.edge_off = k.mask_off + al(8 * TH * tiles);
     k.p_off = k.edge_off + al(4 * 4 * 64 * tiles);
     k.a_off = k.p_off + al(4 * slots);
     k.ent_off = k.a_off + al(4 * slots);
     k.ent_cap = cap;
     k.tile_off = k.ent_off + al(24 * cap);
-    const int64_t total = k.tile_off + al(8 * tiles);
+    const int64_t total = k.tile_off + al((int64_t)sizeof(TileRec) * tiles);
     if (work) *work = k;
     return total;
 }
@@ -814,8 +895,8 @@ extern "C" int ipp_ccl_keep_largest(uint8_t* img, const ipp_image_desc* descs, i
     const int rc =
         run_labels(SRC_ALPHA, img, descs, n_images, max_w, max_h, nullptr, works, scratch, counts, best, bbox, s, L);
     if (rc != IPP_OK) return rc;
-    hipLaunchKernelGGL(k_ccl_apply, L.tile_grid, dim3(256), 0, s, img, descs, works, scratch, best, L.tiles_per_img,
-                       L.tiles_x);
+    hipLaunchKernelGGL(k_ccl_apply, L.group_grid, dim3(64 * WAVES), 0, s, img, descs, works, scratch,
+                       L.groups_per_img, L.groups_x);
     hipLaunchKernelGGL(k_ccl_finish, dim3((n_images + 255) / 256), dim3(256), 0, s, bbox, n_images);
     IPP_CHECK_LAUNCH();
     return IPP_OK;
@@ -837,8 +918,8 @@ extern "C" int ipp_video_keep_largest(const uint8_t* frames, const ipp_image_des
     const int rc =
         run_labels(SRC_HSV, frames, descs, n_images, max_w, max_h, hsv, works, scratch, counts, best, bbox, s, L);
     if (rc != IPP_OK) return rc;
-    hipLaunchKernelGGL(k_ccl_crop_bgr, L.tile_grid, dim3(256), 0, s, frames, descs, works, scratch, best, bbox, out,
-                       out_descs, L.tiles_per_img, L.tiles_x);
+    hipLaunchKernelGGL(k_ccl_crop_bgr, L.group_grid, dim3(64 * WAVES), 0, s, frames, descs, works, scratch, bbox, out,
+                       out_descs, L.groups_per_img, L.groups_x);
     hipLaunchKernelGGL(k_ccl_finish, dim3((n_images + 255) / 256), dim3(256), 0, s, bbox, n_images);
     IPP_CHECK_LAUNCH();
     return IPP_OK;

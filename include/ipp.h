@@ -263,11 +263,13 @@ int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
  * row words of fg bits (tile-major), edge = the global root of each edge
  * pixel (top, bottom, left, right × 64 int32), tile = (first entry, count).
  * P/A: int32/uint32 per run-start index (touched at component roots only);
- * ent: ent_cap {root, area, bbox} records. */
+ * ent: ent_cap {root, area, bbox} records of the components that touch a
+ * tile edge (the others are final after the tile pass). */
 typedef struct ipp_ccl_work {
     int64_t mask_off, edge_off, p_off, a_off, ent_off;
     int64_t ent_cap;
-    int64_t tile_off;
+    int64_t tile_off;   /* per tile: component count, only root, edge flags */
+    int64_t img_off;    /* per image: best closed component, kept root      */
 } ipp_ccl_work;
 
 /* Bytes of scratch for one w×h image; fills *work (may be NULL). */
