@@ -34,7 +34,7 @@
 //                    Written per non-empty tile: the 64 mask words, the root
 //                    of every edge pixel, a record {components, the only
 //                    root, edge flags}.  No per-pixel label plane.
-//   K2 k_ccl_border  one wave per tile: unites the roots of 8-adjacent fg
+//   K2 k_ccl_border  per tile (64 tiles per wave): unites the roots of 8-adjacent fg
 //                    pixel pairs across its right and bottom borders and its
 //                    two lower-right corners (only where both edge flags are
 //                    set), skipping pairs a neighbouring border pixel already
@@ -113,10 +113,16 @@ __device__ __forceinline__ int32_t ld(const int32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ int32_t gfind(const int32_t* P, int32_t x) {
+// Find with path halving: each visited node is re-pointed at its grandparent
+// by a no-return atomicMin (parents only ever decrease), so the chains that
+// concurrent unions build stay short.
+__device__ __forceinline__ int32_t gfind(int32_t* P, int32_t x) {
     int32_t p = ld(P + x);
     while (p != x) {
-        x = p;
+        const int32_t gp = ld(P + p);
+        if (gp == p) return p;
+        __hip_atomic_fetch_min(P + x, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x = gp;
         p = ld(P + x);
     }
     return x;
@@ -516,52 +522,105 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
                                (m0 ? F_TOP : 0) | (m63 ? F_BOT : 0) | (lb ? F_LEFT : 0) | (rbits ? F_RIGHT : 0), 0};
 }
 
-// K2: one wave per tile T unites across its right border (pairs with the
-// tile to the right, rows of one tile row), its bottom border, and the two
-// corner pairs below-right: (63, 63)@T – (0, 0)@T+x+y and (0, 63)@T+x –
-// (63, 0)@T+y.  Along a border, consecutive pixels usually see the same pair
-// of roots: a pair is skipped when the previous (next) pixel with the same
-// near-side root takes it, so a long shared boundary costs one union.
-__device__ __forceinline__ void border_pairs(int32_t* P, const int32_t* near, const int32_t* far, int lane) {
+// K2: per tile T, unions across its right border (pairs with the tile to
+// the right, rows of one tile row), its bottom border, and the two corner
+// pairs below-right: (63, 63)@T – (0, 0)@T+x+y and (0, 63)@T+x – (63, 0)@T+y.
+// One wave takes 64 consecutive tiles: lane i loads the edge flags around tile
+// i, and the wave walks only the borders whose both sides have foreground
+// (launching a wave per tile made the kernel dispatch-bound).  Along a
+// border, consecutive pixels usually see the same pair of roots: a pair is
+// skipped when the previous (next) pixel with the same near-side root takes
+// it, so a long shared boundary costs one union.
+constexpr int ULIST = 256;  // pending unions per wave (LDS), flushed lane-parallel
+
+struct UnionList {
+    int2 u[ULIST];
+};
+
+__device__ __forceinline__ void flush_unions(int32_t* P, UnionList& L, int& n, int lane) {
+    wave_sync();
+    for (int i = lane; i < n; i += 64) gunite(P, L.u[i].x, L.u[i].y);
+    n = 0;
+    wave_sync();
+}
+
+// Appends the (a, c) pairs of the lanes with `want` set (wave-aggregated).
+__device__ __forceinline__ void push_unions(int32_t* P, UnionList& L, int& n, int lane, bool want, int32_t a,
+                                            int32_t c) {
+    const u64 wm = __ballot(want);
+    if (!wm) return;
+    if (n + __popcll(wm) > ULIST) flush_unions(P, L, n, lane);
+    if (want) L.u[n + __popcll(wm & ((1ull << lane) - 1ull))] = make_int2(a, c);
+    n += __popcll(wm);
+}
+
+// One border of 64 pixel pairs (near edge, far edge; lane = position along it).
+__device__ __forceinline__ void border_pairs(int32_t* P, UnionList& L, int& n, const int32_t* near,
+                                             const int32_t* far, int lane) {
     const int32_t a = near[lane];
-    if (a < 0) return;
     const int32_t ap = lane > 0 ? near[lane - 1] : -1, an = lane < 63 ? near[lane + 1] : -1;
     const int32_t cp = lane > 0 ? far[lane - 1] : -1, c0 = far[lane], cn = lane < 63 ? far[lane + 1] : -1;
-    if (cp >= 0 && ap != a) gunite(P, a, cp);
-    if (c0 >= 0 && !(ap == a && cp == c0)) gunite(P, a, c0);
-    if (cn >= 0 && an != a) gunite(P, a, cn);
+    const bool fg = a >= 0;
+    push_unions(P, L, n, lane, fg && cp >= 0 && ap != a, a, cp);
+    push_unions(P, L, n, lane, fg && c0 >= 0 && !(ap == a && cp == c0), a, c0);
+    push_unions(P, L, n, lane, fg && cn >= 0 && an != a, a, cn);
 }
 
 __global__ void __launch_bounds__(64 * WAVES)
 k_ccl_border(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
-             uint8_t* __restrict__ scratch, int groups_per_img, int groups_x) {
+             uint8_t* __restrict__ scratch, int chunks_per_img, int n_images) {
+    __shared__ UnionList lists[WAVES];
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / groups_per_img;
-    const int g = b - im * groups_per_img;
-    const int ty = g / groups_x;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int tx = (g - ty * groups_x) * WAVES + wave;
+    const int cw = (int)b * WAVES + wave;
+    const int im = cw / chunks_per_img;
+    if (im >= n_images) return;  // the grid rounds up to whole blocks
+    const int t = (cw - im * chunks_per_img) * 64 + lane;
     const ipp_image_desc d = descs[im];
     const Frame f = frame_of(d);
-    if (tx >= f.tiles_x || ty >= f.tiles_y) return;
+    const int ntiles = f.tiles_x * f.tiles_y;
+    if ((cw - im * chunks_per_img) * 64 >= ntiles) return;  // wave-uniform
     const Work k = work_of(scratch, works[im]);
-    const int tile = ty * f.tiles_x + tx;
-    const bool has_r = tx + 1 < f.tiles_x, has_b = ty + 1 < f.tiles_y;
-    const int fl = k.tile[tile].flags;
-    const int fr = has_r ? k.tile[tile + 1].flags : 0;
-    const int fb = has_b ? k.tile[tile + f.tiles_x].flags : 0;
-    auto E = [&](int t, int which) { return k.edge + (int64_t)t * (4 * 64) + which * 64; };
-    if ((fl & F_RIGHT) && (fr & F_LEFT)) border_pairs(k.P, E(tile, E_RIGHT), E(tile + 1, E_LEFT), lane);
-    if ((fl & F_BOT) && (fb & F_TOP)) border_pairs(k.P, E(tile, E_BOT), E(tile + f.tiles_x, E_TOP), lane);
-    if (lane == 0 && has_r && has_b) {
-        const int32_t a = (fl & F_BOT) ? E(tile, E_BOT)[63] : -1;
-        const int32_t c = (k.tile[tile + f.tiles_x + 1].flags & F_TOP) ? E(tile + f.tiles_x + 1, E_TOP)[0] : -1;
-        if (a >= 0 && c >= 0) gunite(k.P, a, c);
-        const int32_t a2 = (fr & F_BOT) ? E(tile + 1, E_BOT)[0] : -1;
-        const int32_t c2 = (fb & F_TOP) ? E(tile + f.tiles_x, E_TOP)[63] : -1;
-        if (a2 >= 0 && c2 >= 0) gunite(k.P, a2, c2);
+    UnionList& L = lists[wave];
+    int n = 0;
+    const int ty = t / f.tiles_x, tx = t - ty * f.tiles_x;
+    const bool valid = t < ntiles;
+    const bool has_r = valid && tx + 1 < f.tiles_x, has_b = valid && ty + 1 < f.tiles_y;
+    const int fl = valid ? k.tile[t].flags : 0;
+    const int fr = has_r ? k.tile[t + 1].flags : 0;
+    const int fb = has_b ? k.tile[t + f.tiles_x].flags : 0;
+    const int fd = has_r && has_b ? k.tile[t + f.tiles_x + 1].flags : 0;
+    auto E = [&](int u, int which) { return k.edge + (int64_t)u * (4 * 64) + which * 64; };
+    // corners: lane-parallel, one pair each at most
+    {
+        int32_t a = -1, c = -1;
+        if ((fl & F_BOT) && (fd & F_TOP)) {
+            a = E(t, E_BOT)[63];
+            c = E(t + f.tiles_x + 1, E_TOP)[0];
+        }
+        push_unions(k.P, L, n, lane, a >= 0 && c >= 0, a, c);
+        a = c = -1;
+        if ((fr & F_BOT) && (fb & F_TOP)) {
+            a = E(t + 1, E_BOT)[0];
+            c = E(t + f.tiles_x, E_TOP)[63];
+        }
+        push_unions(k.P, L, n, lane, a >= 0 && c >= 0, a, c);
     }
+    u64 hv = __ballot((fl & F_RIGHT) && (fr & F_LEFT));
+    u64 vv = __ballot((fl & F_BOT) && (fb & F_TOP));
+    const int t0 = t - lane;
+    while (hv) {
+        const int u = t0 + ctz64(hv);
+        border_pairs(k.P, L, n, E(u, E_RIGHT), E(u + 1, E_LEFT), lane);
+        hv &= hv - 1;
+    }
+    while (vv) {
+        const int u = t0 + ctz64(vv);
+        border_pairs(k.P, L, n, E(u, E_BOT), E(u + f.tiles_x, E_TOP), lane);
+        vv &= vv - 1;
+    }
+    flush_unions(k.P, L, n, lane);
 }
 
 // Entry kernels (open components only) run ENT_BLOCKS blocks per image
@@ -803,8 +862,8 @@ __global__ void k_ccl_finish(int32_t* bbox, int n) {
 }
 
 struct Launch {
-    int tiles_x, tiles_y, groups_x, groups_per_img;
-    dim3 group_grid, ent_grid;
+    int tiles_x, tiles_y, groups_x, groups_per_img, chunks_per_img;
+    dim3 group_grid, ent_grid, chunk_grid;
     bool ok;
 };
 
@@ -814,10 +873,13 @@ Launch plan_launch(int n, int max_w, int max_h) {
     L.tiles_y = (max_h + TH - 1) / TH;
     L.groups_x = (L.tiles_x + WAVES - 1) / WAVES;
     L.groups_per_img = L.groups_x * L.tiles_y;
+    L.chunks_per_img = (L.tiles_x * L.tiles_y + 63) / 64;
     const int64_t gb = (int64_t)L.groups_per_img * n, eb = (int64_t)ENT_BLOCKS * n;
-    L.ok = gb < INT32_MAX && eb < INT32_MAX;
+    const int64_t cb = ((int64_t)L.chunks_per_img * n + WAVES - 1) / WAVES;
+    L.ok = gb < INT32_MAX && eb < INT32_MAX && cb < INT32_MAX;
     L.group_grid = dim3((uint32_t)gb);
     L.ent_grid = dim3((uint32_t)eb);
+    L.chunk_grid = dim3((uint32_t)cb);
     return L;
 }
 
@@ -847,8 +909,8 @@ int run_labels(int src, const uint8_t* img, const ipp_image_desc* descs, int32_t
         else if (!zones) launch_label<SRC_HSV, IPP_MAX_HSV_RANGES, false>(L, s, img, descs, works, scratch, counts, q);
         else launch_label<SRC_HSV, IPP_MAX_HSV_RANGES, true>(L, s, img, descs, works, scratch, counts, q);
     }
-    hipLaunchKernelGGL(k_ccl_border, L.group_grid, dim3(64 * WAVES), 0, s, descs, works, scratch, L.groups_per_img,
-                       L.groups_x);
+    hipLaunchKernelGGL(k_ccl_border, L.chunk_grid, dim3(64 * WAVES), 0, s, descs, works, scratch, L.chunks_per_img,
+                       n);
     hipLaunchKernelGGL(k_ccl_resolve, L.ent_grid, dim3(256), 0, s, works, scratch, counts);
     hipLaunchKernelGGL(k_ccl_best, L.ent_grid, dim3(256), 0, s, works, scratch, counts, best);
     hipLaunchKernelGGL(k_ccl_bbox, L.ent_grid, dim3(256), 0, s, descs, works, scratch, counts, best, bbox);
