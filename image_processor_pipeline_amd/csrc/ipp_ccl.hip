@@ -331,6 +331,12 @@ __device__ __forceinline__ void load_rows(const uint8_t* __restrict__ img, const
     }
 }
 
+// v_writelane_b32: lane `lane` of v := s (uniform value and lane).
+extern "C" __device__ int32_t ipp_llvm_writelane(int32_t, int32_t, int32_t) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ void writelane(uint32_t& v, uint32_t s, int lane) {
+    v = (uint32_t)ipp_llvm_writelane((int32_t)s, lane, (int32_t)v);
+}
+
 // Mask words of one tile: lane = column while loading; lane r returns row r's
 // word in m and row r-1's in p.
 template <int SRC, int NR, bool ZONES, bool FULL>
@@ -342,8 +348,7 @@ __device__ __forceinline__ void tile_words(const uint8_t* __restrict__ img, cons
         for (int q = 0; q < NR; ++q) zx |= (uint32_t)((uint32_t)(x - R.c0[q]) < (uint32_t)R.cw[q]) << q;
     }
     const bool xin = x < d.w;
-    m = 0ull;
-    p = 0ull;
+    uint32_t mlo = 0u, mhi = 0u;
     uint32_t bufA[RB], bufB[RB];
     load_rows<SRC, FULL>(img, d, x, y0, bufA);
 #pragma unroll
@@ -369,10 +374,13 @@ __device__ __forceinline__ void tile_words(const uint8_t* __restrict__ img, cons
             }
             if (!FULL) fg = fg && xin && y < d.h;
             const u64 bits = __ballot(fg);
-            m = lane == r ? bits : m;
-            p = lane == r + 1 ? bits : p;
+            writelane(mlo, (uint32_t)bits, r);
+            writelane(mhi, (uint32_t)(bits >> 32), r);
         }
     }
+    m = ((u64)mhi << 32) | mlo;
+    p = __shfl_up(m, 1);
+    p = lane > 0 ? p : 0ull;
 }
 
 // K1: one wave per 64×64 tile, WAVES tiles side by side per block.
@@ -416,6 +424,11 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
         tile_words<SRC, NR, ZONES, true>(img, d, x, y0, lane, Tp, R, m, p);
     else
         tile_words<SRC, NR, ZONES, false>(img, d, x, y0, lane, Tp, R, m, p);
+#ifdef IPP_CCL_DBG_MASK_ONLY  // diagnostic build (wrong output): the mask pass alone
+    if (lane == 0) k.tile[tile] = TileRec{0, -1, 0, 0};
+    if (m == 1ull) k.mask[0] = m;
+    return;
+#endif
     if (__ballot(m != 0ull) == 0ull) {  // no foreground: K2 and K6 skip the tile by its record
         if (lane == 0) k.tile[tile] = TileRec{0, -1, 0, 0};
         return;
@@ -800,15 +813,15 @@ k_ccl_crop_bgr(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int tx = (g - ty * groups_x) * WAVES + wave;
+    // the bbox alone decides most waves (no kept component: an empty bbox)
+    const int bx0 = bbox[4 * im + 0], by0 = bbox[4 * im + 1], bx1 = bbox[4 * im + 2], by1 = bbox[4 * im + 3];
+    const int X0 = tx * TW, Y0 = ty * TH;
+    if (X0 >= bx1 || X0 + TW <= bx0 || Y0 >= by1 || Y0 + TH <= by0) return;
     const ipp_image_desc d = descs[im];
     const Frame f = frame_of(d);
     if (tx >= f.tiles_x || ty >= f.tiles_y) return;
     const Work k = work_of(scratch, works[im]);
     const int32_t broot = k.rec->root;
-    if (broot < 0) return;
-    const int bx0 = bbox[4 * im + 0], by0 = bbox[4 * im + 1], bx1 = bbox[4 * im + 2], by1 = bbox[4 * im + 3];
-    const int X0 = tx * TW, Y0 = ty * TH;
-    if (X0 >= bx1 || X0 + TW <= bx0 || Y0 >= by1 || Y0 + TH <= by0) return;
     const int r0 = max(0, by0 - Y0), r1 = min(TH, by1 - Y0);
     const int x = X0 + lane;
     const bool xin = x >= bx0 && x < bx1;
