@@ -309,9 +309,10 @@ def main(argv=None):
             a_crop = int(sum(max(0, x1 - x0) * max(0, y1 - y0) for x0, y0, x1, y1 in bb))
             hw = B * FH * FW
             # compulsory bytes: read each BGR frame once, write the BGRA crop once
-            # (the uint16 label plane and per-component scratch are reported apart)
+            # (the per-tile mask words and edge roots, 1.5 KB per 64x64 tile at
+            # most, and the per-component scratch are reported apart)
             algo = {"ipp_video_keep_largest": 3 * hw + 4 * a_crop}
-            scratch_bytes = B * (2 * FH * FW)
+            scratch_bytes = B * ((FW + 63) // 64) * ((FH + 63) // 64) * (512 + 1024)
             launches = [("ipp_video_keep_largest", lambda: chain.run(frames))]
 
             def outputs():

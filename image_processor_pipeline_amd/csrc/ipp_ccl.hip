@@ -43,13 +43,14 @@
 //   K4 k_ccl_best    per open root: atomicMax of (area << 32 | ~root).
 //   K5 k_ccl_bbox    the kept component = the better of the open and closed
 //                    bests; bbox from the closed key, or from its entries.
-//   K6 k_ccl_apply / k_ccl_crop_bgr, one wave per tile meeting the output:
+//   K6 k_ccl_apply / k_ccl_inwords, one wave per tile meeting the output:
 //                    a one-component tile takes its mask words or nothing; a
 //                    tile with several relabels its words (the same
 //                    deterministic labelling as K1, so the same ids) and looks
 //                    up each component's final root.  Then α := 0 outside the
-//                    component in place (plugin path), or the crop-fit written
-//                    as BGRA from the BGR frame (fused chain).
+//                    component in place (plugin path), or (fused chain) the
+//                    words are stored and k_ccl_crop_stream writes the crop-fit
+//                    as BGRA from the BGR frame in output-row order.
 // Pixels are read once in K1 and once in K6 (within the crop for the fused
 // chain); everything else is per run, per component or per edge pixel.
 #include <algorithm>
@@ -795,15 +796,18 @@ k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
     }
 }
 
-// K6, fused chain: crop-fit of the BGR frame to the kept component's bbox,
-// written as BGRA (α = 255 inside the component, 0 elsewhere) into the image's
-// output slot; one wave per tile that meets the bbox.  The first rows' pixel
-// loads are issued before the tile's words are worked out.
+// K6, fused chain, in two passes.
+// (a) k_ccl_inwords: one wave per tile that meets the kept component's bbox
+//     overwrites the tile's mask words with its words restricted to the
+//     component (tile_in_word; zeros for tiles without foreground).
+// (b) k_ccl_crop_stream: the crop-fit of the BGR frame written as BGRA (α =
+//     255 inside the component, 0 elsewhere) into the image's output slot,
+//     row by row in output order: 4 pixels per thread (three dword loads, one
+//     16-byte store), so output lines are written whole whatever the bbox's
+//     alignment to the 64-pixel tiles.
 __global__ void __launch_bounds__(64 * WAVES)
-k_ccl_crop_bgr(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
-               const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch,
-               const int32_t* __restrict__ bbox, uint8_t* __restrict__ out,
-               const ipp_image_desc* __restrict__ out_descs, int groups_per_img, int groups_x) {
+k_ccl_inwords(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
+              uint8_t* __restrict__ scratch, const int32_t* __restrict__ bbox, int groups_per_img, int groups_x) {
     __shared__ int par_s[WAVES][NJ];
     __shared__ uint8_t flag_s[WAVES][CMAX];
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
@@ -821,35 +825,82 @@ k_ccl_crop_bgr(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict
     const Frame f = frame_of(d);
     if (tx >= f.tiles_x || ty >= f.tiles_y) return;
     const Work k = work_of(scratch, works[im]);
-    const int32_t broot = k.rec->root;
-    const int r0 = max(0, by0 - Y0), r1 = min(TH, by1 - Y0);
-    const int x = X0 + lane;
-    const bool xin = x >= bx0 && x < bx1;
-    const uint8_t* src = img + d.off + (int64_t)Y0 * d.pitch + 3 * (int64_t)x;
-    const bool last_col = x == d.w - 1;
-    auto load = [&](int r) -> uint32_t {
-        if (!xin) return 0u;
-        const uint8_t* q = src + (int64_t)r * d.pitch;
-        return load_rgb_opaque(q, !last_col || Y0 + r < d.h - 1);
-    };
-    uint32_t px[RB];
-#pragma unroll
-    for (int i = 0; i < RB; ++i) px[i] = r0 + i < r1 ? load(r0 + i) : 0u;
-    const u64 w = tile_in_word(f, k, ty * f.tiles_x + tx, broot, lane, par_s[wave], flag_s[wave], tx, ty);
+    const int tile = ty * f.tiles_x + tx;
+    const u64 w = tile_in_word(f, k, tile, k.rec->root, lane, par_s[wave], flag_s[wave], tx, ty);
+    k.mask[(int64_t)tile * TH + lane] = w;
+}
+
+constexpr int CROP_BLOCKS = 64;  // blocks per image striding over the crop's rows
+
+__global__ void __launch_bounds__(256)
+k_ccl_crop_stream(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
+                  const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch,
+                  const int32_t* __restrict__ bbox, uint8_t* __restrict__ out,
+                  const ipp_image_desc* __restrict__ out_descs) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / CROP_BLOCKS;
+    const int rb = b - im * CROP_BLOCKS;
+    const int bx0 = bbox[4 * im + 0], by0 = bbox[4 * im + 1], bx1 = bbox[4 * im + 2], by1 = bbox[4 * im + 3];
+    if (bx1 <= bx0 || by1 <= by0) return;  // no kept component
+    const ipp_image_desc d = descs[im];
     const ipp_image_desc od = out_descs[im];
-    uint32_t* dst = reinterpret_cast<uint32_t*>(out + od.off) + (x - bx0);
-    for (int rb = r0; rb < r1; rb += RB) {
+    const Frame f = frame_of(d);
+    const Work k = work_of(scratch, works[im]);
+    const int cw = bx1 - bx0;
+    // all (row, 4-pixel chunk) items of the crop, 256 threads × CROP_BLOCKS
+    // blocks striding over them, two items per step for more loads in flight
+    const int cpr = (cw + 3) >> 2;  // chunks per row
+    const int64_t items = (int64_t)cpr * (by1 - by0);
+    const int64_t stride = (int64_t)CROP_BLOCKS * 256;
+    auto item = [&](int64_t it, uint32_t (&o)[4], int& n, uint32_t*& q) {
+        const int oy = (int)(it / cpr), ox = 4 * (int)(it - (int64_t)oy * cpr);
+        const int y = by0 + oy, x = bx0 + ox;
+        n = min(4, cw - ox);
+        const uint8_t* srow = img + d.off + (int64_t)y * d.pitch;
+        const u64* wrow = k.mask + (int64_t)(y / TH) * f.tiles_x * TH + (y & (TH - 1));
+        const u64 w0 = wrow[(int64_t)(x >> 6) * TH];
+        const u64 w1 = ((x + n - 1) >> 6) != (x >> 6) ? wrow[(int64_t)((x + n - 1) >> 6) * TH] : w0;
+        uint32_t px[4];
+        if (n == 4) {
+            const uint8_t* p = srow + 3 * x;
+            const uint32_t d0 = ld_u32_unaligned(p), d1 = ld_u32_unaligned(p + 4), d2 = ld_u32_unaligned(p + 8);
+            px[0] = d0;
+            px[1] = (d0 >> 24) | (d1 << 8);
+            px[2] = (d1 >> 16) | (d2 << 16);
+            px[3] = d2 >> 8;
+        } else {
 #pragma unroll
-        for (int i = 0; i < RB; ++i) {
-            const int r = rb + i;
-            if (r < r1) {
-                const u64 rw = row_word(w, r);
-                if (xin)
-                    *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(dst) + (int64_t)(Y0 + r - by0) * od.pitch) =
-                        (px[i] & 0x00FFFFFFu) | (((rw >> lane) & 1ull) ? 0xFF000000u : 0u);
-                px[i] = r + RB < r1 ? load(r + RB) : 0u;
+            for (int i = 0; i < 4; ++i) {
+                const uint8_t* p = srow + 3 * (x + i);
+                px[i] = i < n ? (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) : 0u;
             }
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int xi = x + i;
+            const u64 w = (xi >> 6) == (x >> 6) ? w0 : w1;
+            o[i] = (px[i] & 0x00FFFFFFu) | (((w >> (xi & 63)) & 1ull) ? 0xFF000000u : 0u);
+        }
+        q = reinterpret_cast<uint32_t*>(out + od.off + (int64_t)oy * od.pitch) + ox;
+    };
+    auto put = [&](const uint32_t (&o)[4], int n, uint32_t* q) {
+        if (n == 4 && ((reinterpret_cast<uintptr_t>(q) & 15u) == 0u)) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<u32x4*>(q) = u32x4{o[0], o[1], o[2], o[3]};
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (i < n) q[i] = o[i];
+        }
+    };
+    for (int64_t it = (int64_t)rb * 256 + threadIdx.x; it < items; it += 2 * stride) {
+        uint32_t oa[4], ob[4];
+        int na, nb = 0;
+        uint32_t *qa, *qb = nullptr;
+        item(it, oa, na, qa);
+        if (it + stride < items) item(it + stride, ob, nb, qb);
+        put(oa, na, qa);
+        if (nb) put(ob, nb, qb);
     }
 }
 
@@ -993,8 +1044,10 @@ extern "C" int ipp_video_keep_largest(const uint8_t* frames, const ipp_image_des
     const int rc =
         run_labels(SRC_HSV, frames, descs, n_images, max_w, max_h, hsv, works, scratch, counts, best, bbox, s, L);
     if (rc != IPP_OK) return rc;
-    hipLaunchKernelGGL(k_ccl_crop_bgr, L.group_grid, dim3(64 * WAVES), 0, s, frames, descs, works, scratch, bbox, out,
-                       out_descs, L.groups_per_img, L.groups_x);
+    hipLaunchKernelGGL(k_ccl_inwords, L.group_grid, dim3(64 * WAVES), 0, s, descs, works, scratch, bbox,
+                       L.groups_per_img, L.groups_x);
+    hipLaunchKernelGGL(k_ccl_crop_stream, dim3((uint32_t)((int64_t)CROP_BLOCKS * n_images)), dim3(256), 0, s, frames,
+                       descs, works, scratch, bbox, out, out_descs);
     hipLaunchKernelGGL(k_ccl_finish, dim3((n_images + 255) / 256), dim3(256), 0, s, bbox, n_images);
     IPP_CHECK_LAUNCH();
     return IPP_OK;
