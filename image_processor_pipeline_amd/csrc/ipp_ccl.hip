@@ -258,7 +258,7 @@ struct TileRec {              // per tile
     int32_t n;                // components in the tile
     int32_t g1;               // root G of the only component when n == 1
     int32_t flags;            // fg on the tile's top / bottom / left / right edge
-    int32_t pad;
+    int32_t g1_open;          // that component touches a tile edge (P holds its root)
 };
 enum { F_TOP = 1, F_BOT = 2, F_LEFT = 4, F_RIGHT = 8 };
 
@@ -441,16 +441,7 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
     const int n = label_tile(par, r, lane, m, p);
     const bool closed_ok = 2ll * f.wb * ((f.h + 1) >> 1) <= CLOSED_SLOTS;
 
-    // P[G] = G at every root (the emit reads P for closed roots too).
-    int32_t g1 = -1;
-    for_runs(m, [&](int a, int) {
-        const int j = slot(r, a);
-        if (par[j] >= NJ) {
-            const int32_t G = slot_gidx(f, tx, ty, j);
-            k.P[G] = G;
-            g1 = G;
-        }
-    });
+    int32_t g1 = -1, g1_open = 0;  // the only component's root (n == 1), for K6
 
     // Stats per component, MAXC ids per pass; open components get entries,
     // closed ones compete for the image's closed key.
@@ -495,6 +486,10 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
             const u64 key = closed_key(ar, G, bx0, by0, bx1, by1);
             best_closed = key > best_closed ? key : best_closed;
         }
+        if (c0 == 0 && lane == 0) {
+            g1 = G;
+            g1_open = open;
+        }
         const u64 om = __ballot(open);
         if (om) {
             int base = 0;
@@ -505,6 +500,7 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
                 k.entL[e] = G;
                 k.entA[e] = ar;
                 k.entB[e] = make_int4(X0 + bx0, y0 + by0, X0 + bx1, y0 + by1);
+                k.P[G] = G;  // open roots only: closed ones never take part in a union
                 k.A[G] = 0u;
             }
         }
@@ -516,24 +512,30 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
     }
     if (lane == 0 && best_closed) atomicMax(&k.rec[0].ckey, best_closed);
 
-    // Edge roots (global G of the pixel's root, -1 for background) and flags.
+    // Edge roots (global G of the pixel's root, -1 for background) of the
+    // edges that hold foreground, and the tile record.
     int32_t* edge = k.edge + (int64_t)tile * (4 * 64);
     const u64 s = m & ~(m << 1);
-    edge[E_LEFT * 64 + lane] = (m & 1ull) ? slot_gidx(f, tx, ty, run_root(par, slot(r, 0))) : -1;
-    edge[E_RIGHT * 64 + lane] = (m >> 63) ? slot_gidx(f, tx, ty, run_root(par, slot(r, 63 - __clzll(s)))) : -1;
     const u64 m0 = __shfl(m, 0), m63 = __shfl(m, TH - 1);
-    const u64 upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-    int32_t t = -1, bo = -1;
-    if ((m0 >> lane) & 1ull) t = slot_gidx(f, tx, ty, run_root(par, slot(0, 63 - __clzll(m0 & ~(m0 << 1) & upto))));
-    if ((m63 >> lane) & 1ull)
-        bo = slot_gidx(f, tx, ty, run_root(par, slot(TH - 1, 63 - __clzll(m63 & ~(m63 << 1) & upto))));
-    edge[E_TOP * 64 + lane] = t;
-    edge[E_BOT * 64 + lane] = bo;
     const u64 lb = __ballot(m & 1ull), rbits = __ballot(m >> 63);
-    g1 = __shfl(g1, 63 - (int)__clzll(__ballot(g1 >= 0) | 1ull));
+    if (lb) edge[E_LEFT * 64 + lane] = (m & 1ull) ? slot_gidx(f, tx, ty, run_root(par, slot(r, 0))) : -1;
+    if (rbits)
+        edge[E_RIGHT * 64 + lane] =
+            (m >> 63) ? slot_gidx(f, tx, ty, run_root(par, slot(r, 63 - __clzll(s)))) : -1;
+    const u64 upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    if (m0)
+        edge[E_TOP * 64 + lane] =
+            ((m0 >> lane) & 1ull) ? slot_gidx(f, tx, ty, run_root(par, slot(0, 63 - __clzll(m0 & ~(m0 << 1) & upto))))
+                                  : -1;
+    if (m63)
+        edge[E_BOT * 64 + lane] =
+            ((m63 >> lane) & 1ull)
+                ? slot_gidx(f, tx, ty, run_root(par, slot(TH - 1, 63 - __clzll(m63 & ~(m63 << 1) & upto))))
+                : -1;
     if (lane == 0)
         k.tile[tile] = TileRec{n, n == 1 ? g1 : -1,
-                               (m0 ? F_TOP : 0) | (m63 ? F_BOT : 0) | (lb ? F_LEFT : 0) | (rbits ? F_RIGHT : 0), 0};
+                               (m0 ? F_TOP : 0) | (m63 ? F_BOT : 0) | (lb ? F_LEFT : 0) | (rbits ? F_RIGHT : 0),
+                               g1_open};
 }
 
 // K2: per tile T, unions across its right border (pairs with the tile to
@@ -738,17 +740,34 @@ k_ccl_bbox(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restr
 // words or nothing; a tile with several relabels its words (same ids as K1)
 // and looks up each component's final root.
 __device__ __forceinline__ u64 tile_in_word(const Frame& f, const Work& k, int tile, int32_t broot, int lane,
-                                            int* par, uint8_t* cflag, int tx, int ty) {
+                                            int* par, uint8_t* cflag, uint32_t* cedge, int tx, int ty) {
     const TileRec t = k.tile[tile];
     if (t.n == 0) return 0ull;
     const u64 m = k.mask[(int64_t)tile * TH + lane];
-    if (t.n == 1) return k.P[t.g1] == broot ? m : 0ull;
+    if (t.n == 1) return (t.g1_open ? k.P[t.g1] == broot : t.g1 == broot) ? m : 0ull;
     const u64 p = __shfl_up(m, 1);
-    label_tile(par, lane, lane, m, lane > 0 ? p : 0ull);
+    const int n = label_tile(par, lane, lane, m, lane > 0 ? p : 0ull);
+    // which components touch a tile edge (open: P holds their root; closed:
+    // the root is their own run-start index, K1's rule)
+    for (int i = lane; i < (n + 31) / 32; i += 64) cedge[i] = 0u;
+    wave_sync();
+    for_runs(m, [&](int a, int len) {
+        if (lane == 0 || lane == TH - 1 || a == 0 || a + len == TW) {
+            const int c = run_cid(par, slot(lane, a));
+            atomicOr(&cedge[c >> 5], 1u << (c & 31));
+        }
+    });
+    wave_sync();
+    const bool closed_ok = 2ll * f.wb * ((f.h + 1) >> 1) <= CLOSED_SLOTS;
     for_runs(m, [&](int a, int) {
         const int j = slot(lane, a);
         const int v = par[j];
-        if (v >= NJ) cflag[v - NJ] = k.P[slot_gidx(f, tx, ty, j)] == broot;
+        if (v >= NJ) {
+            const int c = v - NJ;
+            const int32_t G = slot_gidx(f, tx, ty, j);
+            const bool open = !closed_ok || ((cedge[c >> 5] >> (c & 31)) & 1u);
+            cflag[c] = (open ? k.P[G] : G) == broot;
+        }
     });
     wave_sync();
     u64 w = 0ull;
@@ -771,6 +790,7 @@ k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
             uint8_t* __restrict__ scratch, int groups_per_img, int groups_x) {
     __shared__ int par_s[WAVES][NJ];
     __shared__ uint8_t flag_s[WAVES][CMAX];
+    __shared__ uint32_t cedge_s[WAVES][CMAX / 32];
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int im = b / groups_per_img;
     const int g = b - im * groups_per_img;
@@ -784,7 +804,7 @@ k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
     const Work k = work_of(scratch, works[im]);
     const int32_t broot = k.rec->root;
     if (broot < 0) return;
-    const u64 w = tile_in_word(f, k, ty * f.tiles_x + tx, broot, lane, par_s[wave], flag_s[wave], tx, ty);
+    const u64 w = tile_in_word(f, k, ty * f.tiles_x + tx, broot, lane, par_s[wave], flag_s[wave], cedge_s[wave], tx, ty);
     const int x = tx * TW + lane;
     const int nr = min(TH, d.h - ty * TH);
     for (int r = 0; r < nr; ++r) {
@@ -810,6 +830,7 @@ k_ccl_inwords(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __re
               uint8_t* __restrict__ scratch, const int32_t* __restrict__ bbox, int groups_per_img, int groups_x) {
     __shared__ int par_s[WAVES][NJ];
     __shared__ uint8_t flag_s[WAVES][CMAX];
+    __shared__ uint32_t cedge_s[WAVES][CMAX / 32];
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int im = b / groups_per_img;
     const int g = b - im * groups_per_img;
@@ -826,7 +847,7 @@ k_ccl_inwords(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __re
     if (tx >= f.tiles_x || ty >= f.tiles_y) return;
     const Work k = work_of(scratch, works[im]);
     const int tile = ty * f.tiles_x + tx;
-    const u64 w = tile_in_word(f, k, tile, k.rec->root, lane, par_s[wave], flag_s[wave], tx, ty);
+    const u64 w = tile_in_word(f, k, tile, k.rec->root, lane, par_s[wave], flag_s[wave], cedge_s[wave], tx, ty);
     k.mask[(int64_t)tile * TH + lane] = w;
 }
 
