@@ -109,6 +109,8 @@ struct Hp2Block {
     uint32_t lim;               // CLAMP: last byte offset where a dword fits
     uint32_t rowx, rowy;        // 16.16 source position of column 0 of the lane's row
     int32_t b0, b3, pitch, in_w, in_h;
+    uint32_t rowx8, rowy8;      // SQ8 map: column 0 of row lane>>3 of the band
+    int32_t b1x8, b4x8;         // SQ8 map: +8 rows
     int32_t xlo, xhi;           // band's valid M columns ⊆ [xlo, xhi] (conservative)
 };
 
@@ -144,6 +146,60 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
     }
     o.any = any;
 }
+
+// SQ8 lane map (IPP_HP_SQ8): instruction k gathers the dense 8×8 block at
+// rows 8(k>>1) .. +7, columns 8(k&1) .. +7 of the wave's 16×16 step (lane:
+// row lane>>3, column lane&7), a compact source footprint per instruction;
+// a quad transpose afterwards gives each lane 4 consecutive columns of one
+// row again.  xx/yy = the lane's pixel of instruction 0.
+template <int CN, bool CLAMP>
+__device__ __forceinline__ void hp2_issue_sq8(const Hp2Block& B, uint32_t xx, uint32_t yy, Raw4& o) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t xk = xx + (k & 1) * 8u * (uint32_t)B.b0 + (k >> 1) * (uint32_t)B.b1x8;
+        const uint32_t yk = yy + (k & 1) * 8u * (uint32_t)B.b3 + (k >> 1) * (uint32_t)B.b4x8;
+        const int xin = (int32_t)xk >> 16, yin = (int32_t)yk >> 16;
+        const bool ok = ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h);
+        uint32_t off = (uint32_t)__mul24(yin, B.pitch) + (uint32_t)__umul24((uint32_t)xin, (uint32_t)CN);
+        if (CLAMP) {
+            const uint32_t offc = min(off, B.lim);
+            o.sh[k] = ok ? (off - offc) << 3 : 0u;
+            off = offc;
+        }
+        off = ok ? off : 0xFFFFFFFFu;
+        o.p[k] = __builtin_amdgcn_raw_buffer_load_b32(B.rs, off, 0, 0);
+        any |= ok;
+    }
+    o.any = any;
+}
+
+// 4×4 transpose of dwords across a quad of lanes: lane i of the quad ends
+// with element i of each of the four lanes (element j from lane j).
+__device__ __forceinline__ void quad_transpose4(uint32_t (&a)[4], int lane) {
+    const bool o1 = lane & 1;
+    const uint32_t r0 = __shfl_xor(o1 ? a[0] : a[1], 1), r2 = __shfl_xor(o1 ? a[2] : a[3], 1);
+    if (o1) {
+        a[0] = r0;
+        a[2] = r2;
+    } else {
+        a[1] = r0;
+        a[3] = r2;
+    }
+    const bool o2 = lane & 2;
+    const uint32_t q0 = __shfl_xor(o2 ? a[0] : a[2], 2), q1 = __shfl_xor(o2 ? a[1] : a[3], 2);
+    if (o2) {
+        a[0] = q0;
+        a[1] = q1;
+    } else {
+        a[2] = q0;
+        a[3] = q1;
+    }
+}
+
+#ifndef IPP_HP_SQ8
+#define IPP_HP_SQ8 0
+#endif
 
 // One chunk of ≤ 4 output tiles whose input window fits the ring.
 // Sticky status of the pipe kernels (ipp_pipe_status): bit 0 = an H-pass
@@ -195,9 +251,12 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     int filled = hdr[0].x;  // ring holds M columns [.., filled)
     Hp2Chunk ck = hp2_chunk(hdr, 0, ntiles, filled, wave);
     // Lane's first column of step 0 and its source position.
-    auto lane_x = [&](const Hp2Chunk& c) { return c.c0 + 4 * (wave * 4 + (lane & 3)); };
+    auto lane_x = [&](const Hp2Chunk& c) {
+        return IPP_HP_SQ8 ? c.c0 + 16 * wave + (lane & 7) : c.c0 + 4 * (wave * 4 + (lane & 3));
+    };
+    const uint32_t rx0 = IPP_HP_SQ8 ? B.rowx8 : B.rowx, ry0 = IPP_HP_SQ8 ? B.rowy8 : B.rowy;
     int xl = lane_x(ck);
-    uint32_t xxl = B.rowx + (uint32_t)xl * (uint32_t)B.b0, yyl = B.rowy + (uint32_t)xl * (uint32_t)B.b3;
+    uint32_t xxl = rx0 + (uint32_t)xl * (uint32_t)B.b0, yyl = ry0 + (uint32_t)xl * (uint32_t)B.b3;
     Raw4 RA, RB, RC;
     if (CLAMP) {
 #pragma unroll
@@ -210,8 +269,9 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         return xs + 15 >= B.xlo && xs <= B.xhi;
     };
     auto issue = [&](const Hp2Chunk& c, int st, uint32_t xx, uint32_t yy, int x, Raw4& o) {
-        if (step_live(c, st)) hp2_issue<CN, CLAMP, DBG>(B, xx, yy, x, o);
-        else o.any = false;
+        if (!step_live(c, st)) o.any = false;
+        else if (IPP_HP_SQ8) hp2_issue_sq8<CN, CLAMP>(B, xx, yy, o);
+        else hp2_issue<CN, CLAMP, DBG>(B, xx, yy, x, o);
     };
     if (ck.nsteps > 0) issue(ck, 0, xxl, yyl, xl, RA);
     if (ck.nsteps > 1) issue(ck, 1, xxl + sx, yyl + sy, xl + 64, RB);
@@ -234,18 +294,26 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // rotate so that each step's gathers have two steps of HSV work to land.
         const int c0 = ck.c0, ng4 = ck.ng4, nsteps = ck.nsteps;
         auto process = [&](const Raw4& P, int st) {
-            const int cg = wave * 4 + 16 * st + (lane & 3);
+            // SQ8: after the quad transpose, lane i of quad h (= lane>>2 & 1)
+            // owns row (lane>>3) + 8(i>>1), columns 8(i&1) + 4h .. +3 of the step
+            const int qi = lane & 3;
+            const int cg = IPP_HP_SQ8 ? wave * 4 + 16 * st + 2 * (qi & 1) + ((lane >> 2) & 1)
+                                      : wave * 4 + 16 * st + (lane & 3);
+            const int rw = IPP_HP_SQ8 ? (lane >> 3) + 8 * (qi >> 1) : r;
             const int x = c0 + 4 * cg;
-            const bool active = (cg < ng4) && (r < nrows);
+            const bool active = (cg < ng4) && (rw < nrows);
             uint32_t px[4], zb[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 zb[k] = ~0u;
                 if (ZONES) {
+                    // column of instruction k's pixel (SQ8: before the transpose)
+                    const int xk = IPP_HP_SQ8 ? c0 + 16 * wave + 64 * st + (lane & 7) + 8 * (k & 1) : x + k;
+                    const uint32_t zr = IPP_HP_SQ8 ? ((k >> 1) ? (zrow >> 16) : (zrow & 0xFFFFu)) : zrow;
                     zb[k] = 0;
 #pragma unroll
-                    for (int q = 0; q < NR; ++q) zb[k] |= (uint32_t)((uint32_t)(x + k - zc0[q]) < (uint32_t)zcw[q]) << q;
-                    zb[k] &= zrow;
+                    for (int q = 0; q < NR; ++q) zb[k] |= (uint32_t)((uint32_t)(xk - zc0[q]) < (uint32_t)zcw[q]) << q;
+                    zb[k] &= zr;
                 }
             }
             // One branch per step (not per pixel) so the four pixels' table
@@ -258,10 +326,12 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                     if (CLAMP) raw >>= P.sh[k];
                     px[k] = (DBG & 2) ? (raw | 0x80808080u) : hsv2_px<NR, ZONES>(T, raw, zb[k]);
                 }
+                if (IPP_HP_SQ8) quad_transpose4(px, lane);
                 transpose4(px[0], px[1], px[2], px[3], ch);
             } else if (ZONES) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) px[k] = hsv2_px<NR, ZONES>(T, 0u, zb[k]);
+                if (IPP_HP_SQ8) quad_transpose4(px, lane);
                 transpose4(px[0], px[1], px[2], px[3], ch);
             } else {
 #pragma unroll
@@ -270,7 +340,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             if (active) {
                 const int pos = x & (RING - 1);
 #pragma unroll
-                for (int c = 0; c < 4; ++c) *reinterpret_cast<uint32_t*>(&win[c][r][pos]) = ch[c];
+                for (int c = 0; c < 4; ++c) *reinterpret_cast<uint32_t*>(&win[c][rw][pos]) = ch[c];
             }
         };
         for (int st = 0; st < nsteps; st += 3) {
@@ -290,8 +360,8 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         if (more) {
             ck = hp2_chunk(hdr, s1, ntiles, filled, wave);
             xl = lane_x(ck);
-            xxl = B.rowx + (uint32_t)xl * (uint32_t)B.b0;
-            yyl = B.rowy + (uint32_t)xl * (uint32_t)B.b3;
+            xxl = rx0 + (uint32_t)xl * (uint32_t)B.b0;
+            yyl = ry0 + (uint32_t)xl * (uint32_t)B.b3;
             if (ck.nsteps > 0) issue(ck, 0, xxl, yyl, xl, RA);
             if (ck.nsteps > 1) issue(ck, 1, xxl + sx, yyl + sy, xl + 64, RB);
         }
@@ -455,7 +525,12 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
             int a, bb, cc, dd;
             slice_indices(hp.r[k].zone[0], g.out_h - hp.r[k].zone[1], g.out_h, a, bb);
             slice_indices(hp.r[k].zone[2], g.out_w - hp.r[k].zone[3], g.out_w, cc, dd);
-            zrow |= (uint32_t)(y >= a && y < bb) << k;
+            if (IPP_HP_SQ8) {
+                const int ya = h.line0 + row0 + (lane >> 3), yb = ya + 8;
+                zrow |= ((uint32_t)(ya >= a && ya < bb) << k) | ((uint32_t)(yb >= a && yb < bb) << (16 + k));
+            } else {
+                zrow |= (uint32_t)(y >= a && y < bb) << k;
+            }
             zc0[k] = cc;
             zcw[k] = dd - cc;
         }
@@ -477,6 +552,13 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
     B.rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
     B.b0 = S.b0;
     B.b3 = S.b3;
+    {
+        const int y8 = h.line0 + row0 + (lane >> 3);
+        B.rowx8 = (uint32_t)S.b2 + (uint32_t)y8 * (uint32_t)S.b1;
+        B.rowy8 = (uint32_t)S.b5 + (uint32_t)y8 * (uint32_t)S.b4;
+        B.b1x8 = (int32_t)(8u * (uint32_t)S.b1);
+        B.b4x8 = (int32_t)(8u * (uint32_t)S.b4);
+    }
     B.pitch = (int32_t)S.pitch;
     B.in_w = S.in_w;
     B.in_h = S.in_h;
