@@ -31,7 +31,10 @@ struct TileGrid {
 //          a compact source patch — then each tile is restaged through LDS so
 //          every wave stores 4 full rows (256 B per row per instruction);
 //   ROWS:  wave w covers rows 4w..4w+3 directly (16 lanes × 4 pixels per row).
-constexpr int RT = 4;  // tiles per block (rows of 16)
+#ifndef IPP_ROT_RT
+#define IPP_ROT_RT 4
+#endif
+constexpr int RT = IPP_ROT_RT;  // tiles per block (rows of 16)
 
 template <int CN, bool PATCH, bool DENSE = false>
 __device__ __forceinline__ void rotate_tiles(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
