@@ -32,7 +32,7 @@ struct TileGrid {
 //          every wave stores 4 full rows (256 B per row per instruction);
 //   ROWS:  wave w covers rows 4w..4w+3 directly (16 lanes × 4 pixels per row).
 #ifndef IPP_ROT_RT
-#define IPP_ROT_RT 4
+#define IPP_ROT_RT 2
 #endif
 constexpr int RT = IPP_ROT_RT;  // tiles per block (rows of 16)
 
