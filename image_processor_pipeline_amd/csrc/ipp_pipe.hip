@@ -174,29 +174,6 @@ __device__ __forceinline__ void hp2_issue_sq8(const Hp2Block& B, uint32_t xx, ui
     o.any = any;
 }
 
-// 4×4 transpose of dwords across a quad of lanes: lane i of the quad ends
-// with element i of each of the four lanes (element j from lane j).
-__device__ __forceinline__ void quad_transpose4(uint32_t (&a)[4], int lane) {
-    const bool o1 = lane & 1;
-    const uint32_t r0 = __shfl_xor(o1 ? a[0] : a[1], 1), r2 = __shfl_xor(o1 ? a[2] : a[3], 1);
-    if (o1) {
-        a[0] = r0;
-        a[2] = r2;
-    } else {
-        a[1] = r0;
-        a[3] = r2;
-    }
-    const bool o2 = lane & 2;
-    const uint32_t q0 = __shfl_xor(o2 ? a[0] : a[2], 2), q1 = __shfl_xor(o2 ? a[1] : a[3], 2);
-    if (o2) {
-        a[0] = q0;
-        a[1] = q1;
-    } else {
-        a[2] = q0;
-        a[3] = q1;
-    }
-}
-
 #ifndef IPP_HP_SQ8
 #define IPP_HP_SQ8 0
 #endif
