@@ -184,6 +184,18 @@ __device__ __forceinline__ void hp2_issue_sq8(const Hp2Block& B, uint32_t xx, ui
 // the ring limit of ipp.h; that tile's T columns are wrong).
 __device__ int32_t g_pipe_status;
 
+// Diagnostic builds with -DIPP_HP_STAMPS (and IPP_DIAG): per-wave shader-clock
+// totals of the H-pass phases, summed over the launch (ipp_diag_hp_stamps):
+// [0] phase 1 (gathers, HSV, ring writes, next chunk's issue), [1] barrier
+// before phase 2, [2] phase 2 (MFMA, T stores), [3] barrier after it,
+// [4] waves, [5] chunks, [6] whole body.
+#ifdef IPP_HP_STAMPS
+__device__ unsigned long long g_hp_stamps[8];
+#define HP_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define HP_STAMP(v) const uint64_t v = 0
+#endif
+
 struct Hp2Chunk {
     int s0, s1;   // tiles [s0, s1)
     int c0;       // first M column not yet in the ring
@@ -253,18 +265,24 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     if (ck.nsteps > 0) issue(ck, 0, xxl, yyl, xl, RA);
     if (ck.nsteps > 1) issue(ck, 1, xxl + sx, yyl + sy, xl + 64, RB);
 
+    uint64_t st_p1 = 0, st_b1 = 0, st_p2 = 0, st_b2 = 0, st_n = 0;
+    HP_STAMP(st_begin);
     for (;;) {
+        HP_STAMP(ts0);
         // This wave's tile taps for the first K step, in flight during phase 1.
         const int t = ck.s0 + wave;
         const bool has_tile = !(DBG & 4) && t < ck.s1 && nrows > 0;
         int4 th = make_int4(0, 0, 0, 0);
         uint4 bn[3];
+        int32_t bias = 0;  // the lane's output column bias, in flight with the taps
         const uint4* bt = tblk + lane;
         if (has_tile) {
             th = hdr[t];
             bt += th.z;
 #pragma unroll
             for (int p = 0; p < 3; ++p) bn[p] = bt[p * 64];
+            const int xb = 16 * t + (lane & 15);
+            if (xb < h.out_len) bias = tbias[xb];
         }
 
         // Phase 1: new M columns → planar LDS ring.  Three register sets
@@ -342,7 +360,9 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             if (ck.nsteps > 0) issue(ck, 0, xxl, yyl, xl, RA);
             if (ck.nsteps > 1) issue(ck, 1, xxl + sx, yyl + sy, xl + 64, RB);
         }
+        HP_STAMP(ts1);
         __syncthreads();
+        HP_STAMP(ts2);
 
         // Phase 2 (mfma): wave w takes tile s0 + w; A = 16 window rows × 64
         // columns of one channel (lane l: row l&15, bytes 16(l>>4)..+15),
@@ -375,7 +395,6 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             }
             const int xo = 16 * t + (lane & 15);
             if (xo < h.out_len) {
-                const int32_t bias = tbias[xo];
                 uint32_t outc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
@@ -390,9 +409,30 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                                   outc[3] ^ 0x80808080u);
             }
         }
+        HP_STAMP(ts3);
+        st_p1 += ts1 - ts0;
+        st_b1 += ts2 - ts1;
+        st_p2 += ts3 - ts2;
+        ++st_n;
         if (!more) break;
         __syncthreads();
+        HP_STAMP(ts4);
+        st_b2 += ts4 - ts3;
     }
+#ifdef IPP_HP_STAMPS
+    HP_STAMP(st_end);
+    if (lane == 0) {
+        atomicAdd(&g_hp_stamps[0], (unsigned long long)st_p1);
+        atomicAdd(&g_hp_stamps[1], (unsigned long long)st_b1);
+        atomicAdd(&g_hp_stamps[2], (unsigned long long)st_p2);
+        atomicAdd(&g_hp_stamps[3], (unsigned long long)st_b2);
+        atomicAdd(&g_hp_stamps[4], 1ull);
+        atomicAdd(&g_hp_stamps[5], (unsigned long long)st_n);
+        atomicAdd(&g_hp_stamps[6], (unsigned long long)(st_end - st_begin));
+    }
+#else
+    (void)st_p1; (void)st_b1; (void)st_p2; (void)st_b2; (void)st_n; (void)st_begin;
+#endif
 }
 
 // Composite rows outside the overlay's 16-row bands [vb0, vb1) are plain
@@ -819,6 +859,18 @@ extern "C" int ipp_pipe_hpass_bgcopy(const uint8_t* src, uint8_t* tmp, const int
     return pipe_hpass_impl(src, tmp, coefs, descs, n_images, max_out_w, max_rows, src_cn, hsv, tap_format, bg, dst,
                            stream);
 }
+
+#if defined(IPP_DIAG) && defined(IPP_HP_STAMPS)
+// Diagnostic: reads and clears the H-pass stamp totals (8 × uint64).
+extern "C" int ipp_diag_hp_stamps(unsigned long long* out) {
+    static const unsigned long long zero[8] = {};
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hp_stamps), sizeof(zero), 0, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_hp_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice) != hipSuccess)
+        return IPP_E_LAUNCH;
+    return IPP_OK;
+}
+#endif
 
 extern "C" int ipp_pipe_status(int32_t* status, void* stream) {
     if (!status) return IPP_E_ARG;
