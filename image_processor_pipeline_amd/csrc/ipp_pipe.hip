@@ -177,6 +177,9 @@ __device__ __forceinline__ void hp2_issue_sq8(const Hp2Block& B, uint32_t xx, ui
 #ifndef IPP_HP_SQ8
 #define IPP_HP_SQ8 0
 #endif
+#ifndef IPP_HP_DEPTH  // phase-1 gather depth: steps in flight ahead of the one processed
+#define IPP_HP_DEPTH 2
+#endif
 
 // One chunk of ≤ 4 output tiles whose input window fits the ring.
 // Sticky status of the pipe kernels (ipp_pipe_status): bit 0 = an H-pass
@@ -246,10 +249,10 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     const uint32_t rx0 = IPP_HP_SQ8 ? B.rowx8 : B.rowx, ry0 = IPP_HP_SQ8 ? B.rowy8 : B.rowy;
     int xl = lane_x(ck);
     uint32_t xxl = rx0 + (uint32_t)xl * (uint32_t)B.b0, yyl = ry0 + (uint32_t)xl * (uint32_t)B.b3;
-    Raw4 RA, RB, RC;
+    Raw4 RA, RB, RC, RD;
     if (CLAMP) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) RA.sh[k] = RB.sh[k] = RC.sh[k] = 0u;
+        for (int k = 0; k < 4; ++k) RA.sh[k] = RB.sh[k] = RC.sh[k] = RD.sh[k] = 0u;
     }
     // A step = 16 columns of 16 rows per wave; steps wholly outside the band's
     // valid columns are all fill: no gathers, no HSV, constant window bytes.
@@ -264,6 +267,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     };
     if (ck.nsteps > 0) issue(ck, 0, xxl, yyl, xl, RA);
     if (ck.nsteps > 1) issue(ck, 1, xxl + sx, yyl + sy, xl + 64, RB);
+    if (IPP_HP_DEPTH > 2 && ck.nsteps > 2) issue(ck, 2, xxl + 2 * sx, yyl + 2 * sy, xl + 128, RC);
 
     uint64_t st_p1 = 0, st_b1 = 0, st_p2 = 0, st_b2 = 0, st_n = 0;
     HP_STAMP(st_begin);
@@ -338,15 +342,34 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                 for (int c = 0; c < 4; ++c) *reinterpret_cast<uint32_t*>(&win[c][rw][pos]) = ch[c];
             }
         };
-        for (int st = 0; st < nsteps; st += 3) {
-            if (st + 2 < nsteps) issue(ck, st + 2, xxl + (st + 2) * sx, yyl + (st + 2) * sy, xl + 64 * (st + 2), RC);
-            process(RA, st);
-            if (st + 1 >= nsteps) break;
-            if (st + 3 < nsteps) issue(ck, st + 3, xxl + (st + 3) * sx, yyl + (st + 3) * sy, xl + 64 * (st + 3), RA);
-            process(RB, st + 1);
-            if (st + 2 >= nsteps) break;
-            if (st + 4 < nsteps) issue(ck, st + 4, xxl + (st + 4) * sx, yyl + (st + 4) * sy, xl + 64 * (st + 4), RB);
-            process(RC, st + 2);
+        auto iss = [&](int st2, Raw4& o) {
+            if (st2 < nsteps) issue(ck, st2, xxl + st2 * sx, yyl + st2 * sy, xl + 64 * st2, o);
+        };
+        if (IPP_HP_DEPTH > 2) {  // four register sets: gathers three steps ahead
+            for (int st = 0; st < nsteps; st += 4) {
+                iss(st + 3, RD);
+                process(RA, st);
+                if (st + 1 >= nsteps) break;
+                iss(st + 4, RA);
+                process(RB, st + 1);
+                if (st + 2 >= nsteps) break;
+                iss(st + 5, RB);
+                process(RC, st + 2);
+                if (st + 3 >= nsteps) break;
+                iss(st + 6, RC);
+                process(RD, st + 3);
+            }
+        } else {
+            for (int st = 0; st < nsteps; st += 3) {
+                iss(st + 2, RC);
+                process(RA, st);
+                if (st + 1 >= nsteps) break;
+                iss(st + 3, RA);
+                process(RB, st + 1);
+                if (st + 2 >= nsteps) break;
+                iss(st + 4, RB);
+                process(RC, st + 2);
+            }
         }
 
         // Next chunk's first two steps: their gathers fly during phase 2.
@@ -359,6 +382,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             yyl = ry0 + (uint32_t)xl * (uint32_t)B.b3;
             if (ck.nsteps > 0) issue(ck, 0, xxl, yyl, xl, RA);
             if (ck.nsteps > 1) issue(ck, 1, xxl + sx, yyl + sy, xl + 64, RB);
+            if (IPP_HP_DEPTH > 2 && ck.nsteps > 2) issue(ck, 2, xxl + 2 * sx, yyl + 2 * sy, xl + 128, RC);
         }
         HP_STAMP(ts1);
         __syncthreads();
