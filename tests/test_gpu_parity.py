@@ -278,6 +278,41 @@ def test_pipe_crop_reaching_source_end(D):
             assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (margins, i)
 
 
+def test_pipe_edge_parameters_vs_oracle(D):
+    """Explicit item parameters at the edges of their ranges: Pillow's
+    right-angle fast paths (0/90/180/270 and their wraps) under every flip,
+    overlays pasted flush with each background border, the smallest and the
+    largest overlay ratios (the largest capped by the background height,
+    overlays.py:106-126), and items sharing one background."""
+    from image_processor_pipeline_amd import fused
+    from image_processor_pipeline_amd import geometry as G
+    cfg = fused.PipeConfig(margins=(6, 4, 2, 8))
+    H, W, bh, bw, K = 96, 130, 120, 150, 2
+    rng = np.random.default_rng(41)
+    angles = [0.0, 90.0, 180.0, 270.0, 450.0, -90.0, 1.0, 359.0, 45.0, 135.0]
+    syms = ["o", "h", "v", "hv", "hv", "v", "h", "o", "v", "h"]
+    ratios = [0.05, 1.0, 0.5, 0.3, 0.9, 0.15, 0.7, 0.2, 1.0, 0.1]
+    n = len(angles)
+    src = rng.integers(0, 256, (n, H, W, 3), np.uint8)
+    bgs = rng.integers(0, 256, (K, bh, bw, 3), np.uint8)
+    params = []
+    for i in range(n):
+        p = fused.ItemParams(angle=angles[i], sym=syms[i], bg_index=i % K, ratio=ratios[i])
+        mt, mb, ml, mr = G.crop_margins(H, W, cfg.margins)
+        _, _, (nw, nh) = fused.item_geometry(W - ml - mr, H - mt - mb, angles[i], ratios[i], bw, bh, i)
+        corner = i % 4  # flush with the left/top, right/top, left/bottom, right/bottom borders
+        p.x = 0 if corner in (0, 2) else bw - nw
+        p.y = 0 if corner in (0, 1) else bh - nh
+        params.append(p)
+    plan = fused.plan_pipe((H, W), n, (bh, bw), K, cfg, params=params)
+    runner = fused.PipeRunner(plan, DEV)
+    out = torch.empty((n, bh, bw, 3), dtype=torch.uint8, device=DEV)
+    runner.run(_t(src), _t(bgs), out)
+    got = out.cpu().numpy()
+    for i in range(n):
+        assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (i, angles[i], syms[i])
+
+
 def test_pipe_fullsize_items_vs_oracle(D):
     """BASELINE config 3 geometry (1024² sources, 64-px margins, 1024² bgs)."""
     from image_processor_pipeline_amd import fused
