@@ -31,7 +31,15 @@ namespace {
 
 constexpr int HR = 16;            // H-pass rows per block (4 per thread)
 constexpr int RING = 512;         // window ring: M columns x live at x & (RING - 1)
-constexpr int WSTRIDE = 528;      // LDS bytes per plane row (≡ 4 dwords mod 32 banks)
+// LDS bytes per plane row of the window ring.  544 ≡ 8 dwords mod 64 banks:
+// the phase-2 ds_read_b128 (4 lane groups of 16, 4 dwords each) then covers
+// 64 distinct banks per group, and the phase-1 ds_write_b32 rows pair up 2-way,
+// which a dword store absorbs (MI355X_MICROARCH.md §LDS).  (528 left the
+// b128 reads 2-way; measured the same time, the pass is not LDS-bound.)
+#ifndef IPP_HP_WSTRIDE
+#define IPP_HP_WSTRIDE 544
+#endif
+constexpr int WSTRIDE = IPP_HP_WSTRIDE;
 // ipp_pipe_hpass_bgcopy: background-copy blocks per item.  Diagnostic builds
 // (-DIPP_DIAG) may override it and select the experiment kernels below through
 // environment variables; the product build reads no environment at all.
