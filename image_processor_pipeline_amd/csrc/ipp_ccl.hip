@@ -851,7 +851,10 @@ k_ccl_inwords(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __re
     k.mask[(int64_t)tile * TH + lane] = w;
 }
 
-constexpr int CROP_BLOCKS = 64;  // blocks per image striding over the crop's rows
+#ifndef IPP_CCL_CROP_BLOCKS
+#define IPP_CCL_CROP_BLOCKS 256
+#endif
+constexpr int CROP_BLOCKS = IPP_CCL_CROP_BLOCKS;  // blocks per image striding over the crop
 
 __global__ void __launch_bounds__(256)
 k_ccl_crop_stream(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
