@@ -145,11 +145,15 @@ __device__ __forceinline__ void gunite(int32_t* P, int32_t a, int32_t b) {
     }
 }
 
-__device__ __forceinline__ int lld(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
+// Per-wave LDS union-find over run slots, 16-bit entries (slots < NJ, and
+// NJ + component id < NJ + CMAX after label_tile): 4 KB per wave.  A union's
+// atomicMin is a 32-bit compare-and-swap on the word holding the entry (LDS
+// has no 16-bit atomics); plain 16-bit loads and stores elsewhere.
+typedef uint16_t Par;
 
-__device__ __forceinline__ int lfind(const int* par, int x) {
+__device__ __forceinline__ int lld(const Par* p) { return *reinterpret_cast<const volatile Par*>(p); }
+
+__device__ __forceinline__ int lfind(const Par* par, int x) {
     int p = lld(par + x);
     while (p != x) {
         x = p;
@@ -158,7 +162,22 @@ __device__ __forceinline__ int lfind(const int* par, int x) {
     return x;
 }
 
-__device__ __forceinline__ void lunite(int* par, int a, int b) {
+// par[b] = min(par[b], a); returns the previous par[b].
+__device__ __forceinline__ int lmin16(Par* par, int b, int a) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(par + (b & ~1));
+    const int sh = (b & 1) * 16;
+    uint32_t cur = *reinterpret_cast<volatile uint32_t*>(w);
+    for (;;) {
+        const int old = (int)((cur >> sh) & 0xFFFFu);
+        if (old <= a) return old;
+        const uint32_t nw = (cur & ~(0xFFFFu << sh)) | ((uint32_t)a << sh);
+        const uint32_t prev = atomicCAS(w, cur, nw);
+        if (prev == cur) return old;
+        cur = prev;
+    }
+}
+
+__device__ __forceinline__ void lunite(Par* par, int a, int b) {
     for (;;) {
         a = lfind(par, a);
         b = lfind(par, b);
@@ -168,7 +187,7 @@ __device__ __forceinline__ void lunite(int* par, int a, int b) {
             a = b;
             b = t;
         }
-        const int old = __hip_atomic_fetch_min(par + b, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const int old = lmin16(par, b, a);
         if (old == b) return;
         b = old;
     }
@@ -198,7 +217,7 @@ __device__ __forceinline__ int wave_scan_excl(int v, int lane, int& total) {
 // any other run its root's slot; returns the component count.  Component ids
 // follow (row, run) order — a pure function of the words, so K6 relabelling a
 // tile reproduces K1's ids.
-__device__ __forceinline__ int label_tile(int* par, int r, int lane, u64 m, u64 p) {
+__device__ __forceinline__ int label_tile(Par* par, int r, int lane, u64 m, u64 p) {
     for_runs(m, [&](int a, int) { par[slot(r, a)] = slot(r, a); });
     wave_sync();
     if (p) {
@@ -238,11 +257,11 @@ __device__ __forceinline__ int label_tile(int* par, int r, int lane, u64 m, u64 
     return n;
 }
 
-__device__ __forceinline__ int run_root(const int* par, int j) {
+__device__ __forceinline__ int run_root(const Par* par, int j) {
     const int v = par[j];
     return v >= NJ ? j : v;
 }
-__device__ __forceinline__ int run_cid(const int* par, int j) {
+__device__ __forceinline__ int run_cid(const Par* par, int j) {
     const int v = par[j];
     return (v >= NJ ? v : par[v]) - NJ;
 }
@@ -390,7 +409,7 @@ __global__ void __launch_bounds__(64 * WAVES)
 k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
             const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, int32_t* __restrict__ counts,
             int groups_per_img, int groups_x, ipp_hsv_params hp) {
-    __shared__ int par_s[WAVES][NJ];
+    __shared__ Par par_s[WAVES][NJ];
     __shared__ uint32_t st_area[WAVES][MAXC];
     __shared__ u64 st_rows[WAVES][MAXC], st_cols[WAVES][MAXC];
     __shared__ int st_root[WAVES][MAXC];
@@ -412,7 +431,7 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
         __syncthreads();
     }
     if (tx >= f.tiles_x || ty >= f.tiles_y) return;  // wave-uniform; no barrier follows
-    int* par = par_s[wave];
+    Par* par = par_s[wave];
     const Work k = work_of(scratch, works[im]);
     const int x = tx * TW + lane, y0 = ty * TH, X0 = tx * TW;
     const int tile = ty * f.tiles_x + tx;
@@ -740,7 +759,7 @@ k_ccl_bbox(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restr
 // words or nothing; a tile with several relabels its words (same ids as K1)
 // and looks up each component's final root.
 __device__ __forceinline__ u64 tile_in_word(const Frame& f, const Work& k, int tile, int32_t broot, int lane,
-                                            int* par, uint8_t* cflag, uint32_t* cedge, int tx, int ty) {
+                                            Par* par, uint8_t* cflag, uint32_t* cedge, int tx, int ty) {
     const TileRec t = k.tile[tile];
     if (t.n == 0) return 0ull;
     const u64 m = k.mask[(int64_t)tile * TH + lane];
@@ -788,7 +807,7 @@ __device__ __forceinline__ u64 row_word(u64 w, int r) {
 __global__ void __launch_bounds__(64 * WAVES)
 k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
             uint8_t* __restrict__ scratch, int groups_per_img, int groups_x) {
-    __shared__ int par_s[WAVES][NJ];
+    __shared__ Par par_s[WAVES][NJ];
     __shared__ uint8_t flag_s[WAVES][CMAX];
     __shared__ uint32_t cedge_s[WAVES][CMAX / 32];
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
@@ -828,7 +847,7 @@ k_ccl_apply(uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
 __global__ void __launch_bounds__(64 * WAVES)
 k_ccl_inwords(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
               uint8_t* __restrict__ scratch, const int32_t* __restrict__ bbox, int groups_per_img, int groups_x) {
-    __shared__ int par_s[WAVES][NJ];
+    __shared__ Par par_s[WAVES][NJ];
     __shared__ uint8_t flag_s[WAVES][CMAX];
     __shared__ uint32_t cedge_s[WAVES][CMAX / 32];
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
