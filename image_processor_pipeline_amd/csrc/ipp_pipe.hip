@@ -73,7 +73,22 @@ __device__ __forceinline__ void transpose4(uint32_t p0, uint32_t p1, uint32_t p2
     ch[3] = perm(hi23, hi01, 0x07060302u);
 }
 
+// Q22 lane pair (dx = lane & 1) holding columns {dx, dx + 2, dx + 4, dx + 6}
+// of one row → lane 0 holds columns 0..3, lane 1 columns 4..7 (two DPP
+// swaps with the partner lane).
+__device__ __forceinline__ void pair_regroup(uint32_t (&a)[4], bool o1) {
+    const uint32_t s0 = o1 ? a[0] : a[2], s1 = o1 ? a[1] : a[3];
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s0, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0xB1, 0xF, 0xF, false);
+    const uint32_t b0 = o1 ? r0 : a[0], b1 = o1 ? a[2] : r0, b2 = o1 ? r1 : a[1], b3 = o1 ? a[3] : r1;
+    a[0] = b0;
+    a[1] = b1;
+    a[2] = b2;
+    a[3] = b3;
+}
+
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
 // H pass v2 (MFMA taps): table-driven HSV test and buffer-load gathers.
@@ -114,6 +129,7 @@ __device__ __forceinline__ uint32_t hsv2_px(const HsvTables<NR>& T, uint32_t raw
 // Per-block state of the v2 H pass.
 struct Hp2Block {
     __amdgpu_buffer_rsrc_t rs;  // source window (records = bytes to the image end)
+    u32x4_t rsv;                // the same descriptor as four dwords (IPP_HP_ASMG)
     uint32_t lim;               // CLAMP: last byte offset where a dword fits
     uint32_t rowx, rowy;        // 16.16 source position of column 0 of the lane's row
     int32_t b0, b3, pitch, in_w, in_h;
@@ -127,32 +143,90 @@ struct Raw4 {
     uint32_t p[4];
     uint32_t sh[4];
     bool any;
+    bool live;  // IPP_HP_ASMG: the step's loads were issued (block-uniform)
 };
 
+// IPP_HP_ASMG: the gathers are issued by inline asm and waited for by hand.
+// The compiler then neither counts them (its vmcnt bookkeeping merges paths
+// pessimistically, so a step skipped on some path made every later wait drain
+// the gathers issued for the steps ahead) nor copies their registers (a copy
+// of a register whose load is in flight would wait for it).  Dead steps issue
+// nothing; a set is waited for with vmcnt(4 × live sets issued after it),
+// which never exceeds the loads really issued after it (compiler-issued loads
+// in between only make the wait stricter).  The wait names the four data
+// registers as in/out operands, so no use of them can move above it.
+#ifndef IPP_HP_ASMG
+#define IPP_HP_ASMG 1
+#endif
+__device__ __forceinline__ uint32_t asm_gather(u32x4_t rs, uint32_t off) {
+    uint32_t v;
+    asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(rs));
+    return v;
+}
+// One asm statement on every path (newer = 8, 4, 0, or -1: the set was not
+// issued, no wait): with a wait per path the compiler merged the paths through
+// register copies, which read the data registers before their loads landed.
+__device__ __forceinline__ void asm_wait(uint32_t (&p)[4], int32_t newer) {
+    asm volatile(
+        "s_cmp_eq_u32 %4, 8\n\t"
+        "s_cbranch_scc0 1f\n\t"
+        "s_waitcnt vmcnt(8)\n\t"
+        "s_branch 4f\n"
+        "1:\n\t"
+        "s_cmp_eq_u32 %4, 4\n\t"
+        "s_cbranch_scc0 2f\n\t"
+        "s_waitcnt vmcnt(4)\n\t"
+        "s_branch 4f\n"
+        "2:\n\t"
+        "s_cmp_eq_u32 %4, 0\n\t"
+        "s_cbranch_scc0 4f\n\t"
+        "s_waitcnt vmcnt(0)\n"
+        "4:"
+        : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3])
+        : "s"(newer)
+        : "scc");
+}
+
 // Gathers of one step: xx/yy = 16.16 source position of the lane's first
-// pixel (its next three are +b0/+b3 apart).
-template <int CN, bool CLAMP, int DBG = 0>
-__device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32_t yy, int x, Raw4& o) {
+// pixel (its next three are XSTEP columns apart).  Out-of-window pixels load
+// offset 0xFFFFFFFF (the range check returns 0).  A dead step (live == false)
+// is only reached with IPP_HP_LIVESKIP = 0 and IPP_HP_ASMG = 0: it loads all
+// lanes out of range, which keeps the compiler's vmcnt count exact but costs
+// the texture path as much as real loads (+9 %, measured).
+template <int CN, bool CLAMP, int DBG = 0, int XSTEP = 1>
+__device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32_t yy, int x, bool live, Raw4& o) {
     bool any = false;
+    uint32_t off[4];
+    if (live) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int xin = (int32_t)xx >> 16, yin = (int32_t)yy >> 16;
-        const bool ok = ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h);
-        uint32_t off = (uint32_t)__mul24(yin, B.pitch) + (uint32_t)__umul24((uint32_t)xin, (uint32_t)CN);
-        if (CLAMP) {
-            const uint32_t offc = min(off, B.lim);
-            o.sh[k] = ok ? (off - offc) << 3 : 0u;
-            off = offc;
+        for (int k = 0; k < 4; ++k) {
+            const int xin = (int32_t)xx >> 16, yin = (int32_t)yy >> 16;
+            const bool ok = ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h);
+            uint32_t o1 = (uint32_t)__mul24(yin, B.pitch) + (uint32_t)__umul24((uint32_t)xin, (uint32_t)CN);
+            if (CLAMP) {
+                const uint32_t offc = min(o1, B.lim);
+                o.sh[k] = ok ? (o1 - offc) << 3 : 0u;
+                o1 = offc;
+            }
+            if (DBG & 1) o1 = (uint32_t)((x >> 6) * 768 + (threadIdx.x & 63) * 3 + k * 192 + (threadIdx.x >> 8) * 3072);
+            if (DBG & 16) o1 &= 0x7FFFu;  // same scatter, 32 KiB footprint (cache-resident)
+            off[k] = ok ? o1 : 0xFFFFFFFFu;
+            any |= ok;
+            xx += (uint32_t)(XSTEP * B.b0);
+            yy += (uint32_t)(XSTEP * B.b3);
         }
-        if (DBG & 1) off = (uint32_t)((x >> 6) * 768 + (threadIdx.x & 63) * 3 + k * 192 + (threadIdx.x >> 8) * 3072);
-        if (DBG & 16) off &= 0x7FFFu;  // same scatter, 32 KiB footprint (cache-resident)
-        off = ok ? off : 0xFFFFFFFFu;
-        o.p[k] = __builtin_amdgcn_raw_buffer_load_b32(B.rs, off, 0, 0);
-        any |= ok;
-        xx += (uint32_t)B.b0;
-        yy += (uint32_t)B.b3;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            off[k] = 0xFFFFFFFFu;
+            if (CLAMP) o.sh[k] = 0u;
+        }
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        o.p[k] = IPP_HP_ASMG ? asm_gather(B.rsv, off[k]) : __builtin_amdgcn_raw_buffer_load_b32(B.rs, off[k], 0, 0);
     o.any = any;
+    o.live = true;
 }
 
 // SQ8 lane map (IPP_HP_SQ8): instruction k gathers the dense 8×8 block at
@@ -161,33 +235,72 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
 // a quad transpose afterwards gives each lane 4 consecutive columns of one
 // row again.  xx/yy = the lane's pixel of instruction 0.
 template <int CN, bool CLAMP>
-__device__ __forceinline__ void hp2_issue_sq8(const Hp2Block& B, uint32_t xx, uint32_t yy, Raw4& o) {
+__device__ __forceinline__ void hp2_issue_sq8(const Hp2Block& B, uint32_t xx, uint32_t yy, bool live, Raw4& o) {
     bool any = false;
+    uint32_t off[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t xk = xx + (k & 1) * 8u * (uint32_t)B.b0 + (k >> 1) * (uint32_t)B.b1x8;
         const uint32_t yk = yy + (k & 1) * 8u * (uint32_t)B.b3 + (k >> 1) * (uint32_t)B.b4x8;
         const int xin = (int32_t)xk >> 16, yin = (int32_t)yk >> 16;
-        const bool ok = ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h);
-        uint32_t off = (uint32_t)__mul24(yin, B.pitch) + (uint32_t)__umul24((uint32_t)xin, (uint32_t)CN);
+        const bool ok = live & ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h);
+        uint32_t o1 = (uint32_t)__mul24(yin, B.pitch) + (uint32_t)__umul24((uint32_t)xin, (uint32_t)CN);
         if (CLAMP) {
-            const uint32_t offc = min(off, B.lim);
-            o.sh[k] = ok ? (off - offc) << 3 : 0u;
-            off = offc;
+            const uint32_t offc = min(o1, B.lim);
+            o.sh[k] = ok ? (o1 - offc) << 3 : 0u;
+            o1 = offc;
         }
-        off = ok ? off : 0xFFFFFFFFu;
-        o.p[k] = __builtin_amdgcn_raw_buffer_load_b32(B.rs, off, 0, 0);
+        off[k] = ok ? o1 : 0xFFFFFFFFu;
         any |= ok;
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o.p[k] = __builtin_amdgcn_raw_buffer_load_b32(B.rs, off[k], 0, 0);
     o.any = any;
+    o.live = true;
 }
 
 #ifndef IPP_HP_SQ8
 #define IPP_HP_SQ8 0
 #endif
+// Gather lane map.  0: lane quad = 4 column groups of one row (instruction k
+// takes column 4q + k), so a quad's 4 pixels lie 4 columns apart.  1 (Q22):
+// lane quad = a 2×2 block of M pixels (instruction k takes columns 2k + dx of
+// rows 2g' + dy), whose source pixels lie within ~1.5 pixels of each other.
+// A lane-pair exchange afterwards gives each lane 4 consecutive columns of
+// its row again.  Measured on the box: 1.7 % faster than map 0, although the
+// L1 tag lookups per gather instruction rose from 65 to 76
+// (TCP_TOTAL_CACHE_ACCESSES / TA_BUFFER_READ_WAVEFRONTS).
+#ifndef IPP_HP_Q22
+#define IPP_HP_Q22 1
+#endif
+// Dead steps (past the chunk or wholly fill) skip their gather loads (1) or
+// issue them out of range (0: exact vmcnt waits, but the texture path still
+// processes every lane).
+#ifndef IPP_HP_LIVESKIP
+#define IPP_HP_LIVESKIP 1
+#endif
+// Next chunk's first gathers: 0 after phase 2, 1 before it (before the
+// barrier), 2 after its MFMAs (before the T store).
+#ifndef IPP_HP_NEXT_EARLY
+#define IPP_HP_NEXT_EARLY 1
+#endif
 #ifndef IPP_HP_DEPTH  // phase-1 gather depth: steps in flight ahead of the one processed
 #define IPP_HP_DEPTH 2
 #endif
+// Waves per H-pass block (one 16-row band).  4: wave w owns tile s0 + w of a
+// chunk, all 16 rows × 4 channels (48 accumulator registers).  8: wave w owns
+// tile s0 + (w & 3), rows 8(w >> 2) .. +7; its MFMA A rows are (channel, row)
+// pairs of a 4-row group, so two row groups × 3 byte planes need 24
+// accumulators and the block's phase-1 columns spread over twice the waves.
+#ifndef IPP_HP_NW
+#define IPP_HP_NW 4
+#endif
+constexpr int HP_NW = IPP_HP_NW;
+constexpr int HP_STEPC = 16 * HP_NW;  // M columns per block-wide phase-1 step
+static_assert(HP_NW == 4 || HP_NW == 8, "IPP_HP_NW: 4 or 8 waves per band");
+static_assert(!(IPP_HP_SQ8 && HP_NW != 4), "the SQ8 gather map assumes 4 waves per band");
+static_assert(!(IPP_HP_SQ8 && IPP_HP_Q22), "one gather lane map");
+static_assert(!(IPP_HP_SQ8 && IPP_HP_ASMG), "the SQ8 gather map uses compiler-tracked loads");
 
 // One chunk of ≤ 4 output tiles whose input window fits the ring.
 // Sticky status of the pipe kernels (ipp_pipe_status): bit 0 = an H-pass
@@ -229,7 +342,7 @@ __device__ __forceinline__ Hp2Chunk hp2_chunk(const int4* hdr, int s0, int ntile
     if (W1 - W0 > RING && threadIdx.x == 0) atomicOr(&g_pipe_status, 1);  // single tile beyond the ring
     c.c0 = max(filled, W0);
     c.ng4 = max(0, (W1 - c.c0) >> 2);
-    c.nsteps = c.ng4 > wave * 4 ? (c.ng4 - wave * 4 + 15) >> 4 : 0;
+    c.nsteps = c.ng4 > wave * 4 ? (c.ng4 - wave * 4 + 4 * HP_NW - 1) / (4 * HP_NW) : 0;
     filled = max(filled, W1);
     return c;
 }
@@ -241,23 +354,26 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                                             int row0, int nrows, const int32_t* zc0, const int32_t* zcw,
                                             uint32_t zrow, uint32_t fill) {
     const int lane = threadIdx.x & 63;
-    const int r = lane >> 2;
+    const int r = IPP_HP_Q22 ? 2 * (lane >> 3) + ((lane >> 1) & 1) : lane >> 2;  // the lane's window row
     const int ntiles = (h.out_len + 15) >> 4;
     const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
     const int32_t* tbias = coefs + h.coef_off + 4 * (int64_t)ntiles;
     const uint4* tblk = reinterpret_cast<const uint4*>(coefs + h.coef_off + 20 * (int64_t)ntiles);
-    const uint32_t sx = 64u * (uint32_t)B.b0, sy = 64u * (uint32_t)B.b3;  // per-step advance
+    const uint32_t sx = (uint32_t)HP_STEPC * (uint32_t)B.b0, sy = (uint32_t)HP_STEPC * (uint32_t)B.b3;  // per-step advance
 
     int filled = hdr[0].x;  // ring holds M columns [.., filled)
     Hp2Chunk ck = hp2_chunk(hdr, 0, ntiles, filled, wave);
     // Lane's first column of step 0 and its source position.
     auto lane_x = [&](const Hp2Chunk& c) {
-        return IPP_HP_SQ8 ? c.c0 + 16 * wave + (lane & 7) : c.c0 + 4 * (wave * 4 + (lane & 3));
+        return IPP_HP_SQ8   ? c.c0 + 16 * wave + (lane & 7)
+               : IPP_HP_Q22 ? c.c0 + 16 * wave + 8 * ((lane >> 2) & 1) + (lane & 1)
+                            : c.c0 + 4 * (wave * 4 + (lane & 3));
     };
     const uint32_t rx0 = IPP_HP_SQ8 ? B.rowx8 : B.rowx, ry0 = IPP_HP_SQ8 ? B.rowy8 : B.rowy;
     int xl = lane_x(ck);
     uint32_t xxl = rx0 + (uint32_t)xl * (uint32_t)B.b0, yyl = ry0 + (uint32_t)xl * (uint32_t)B.b3;
     Raw4 RA, RB, RC, RD;
+    RA.live = RB.live = RC.live = RD.live = false;
     if (CLAMP) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) RA.sh[k] = RB.sh[k] = RC.sh[k] = RD.sh[k] = 0u;
@@ -265,47 +381,63 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     // A step = 16 columns of 16 rows per wave; steps wholly outside the band's
     // valid columns are all fill: no gathers, no HSV, constant window bytes.
     auto step_live = [&](const Hp2Chunk& c, int st) {
-        const int xs = c.c0 + 16 * wave + 64 * st;
+        const int xs = c.c0 + 16 * wave + HP_STEPC * st;
         return xs + 15 >= B.xlo && xs <= B.xhi;
     };
+    // Every call issues its four loads (dead steps included, see hp2_issue),
+    // so the vmcnt waits stay exact between a step's issue and its use.
     auto issue = [&](const Hp2Chunk& c, int st, uint32_t xx, uint32_t yy, int x, Raw4& o) {
-        if (!step_live(c, st)) o.any = false;
-        else if (IPP_HP_SQ8) hp2_issue_sq8<CN, CLAMP>(B, xx, yy, o);
-        else hp2_issue<CN, CLAMP, DBG>(B, xx, yy, x, o);
+        const bool live = st < c.nsteps && step_live(c, st);
+        if ((IPP_HP_LIVESKIP || IPP_HP_ASMG) && !live) {
+            o.any = false;
+            o.live = false;
+            return;
+        }
+        if (IPP_HP_SQ8) hp2_issue_sq8<CN, CLAMP>(B, xx, yy, live, o);
+        else hp2_issue<CN, CLAMP, DBG, IPP_HP_Q22 ? 2 : 1>(B, xx, yy, x, live, o);
     };
-    if (ck.nsteps > 0) issue(ck, 0, xxl, yyl, xl, RA);
-    if (ck.nsteps > 1) issue(ck, 1, xxl + sx, yyl + sy, xl + 64, RB);
-    if (IPP_HP_DEPTH > 2 && ck.nsteps > 2) issue(ck, 2, xxl + 2 * sx, yyl + 2 * sy, xl + 128, RC);
+    issue(ck, 0, xxl, yyl, xl, RA);
+    issue(ck, 1, xxl + sx, yyl + sy, xl + HP_STEPC, RB);
+    if (IPP_HP_DEPTH > 2) issue(ck, 2, xxl + 2 * sx, yyl + 2 * sy, xl + 2 * HP_STEPC, RC);
 
     uint64_t st_p1 = 0, st_b1 = 0, st_p2 = 0, st_b2 = 0, st_n = 0;
     HP_STAMP(st_begin);
     for (;;) {
         HP_STAMP(ts0);
         // This wave's tile taps for the first K step, in flight during phase 1.
-        const int t = ck.s0 + wave;
+        const int t = ck.s0 + (wave & 3);
         const bool has_tile = !(DBG & 4) && t < ck.s1 && nrows > 0;
         int4 th = make_int4(0, 0, 0, 0);
         uint4 bn[3];
         int32_t bias = 0;  // the lane's output column bias, in flight with the taps
         const uint4* bt = tblk + lane;
-        if (has_tile) {
-            th = hdr[t];
+        {
+            // Loaded unconditionally (a valid tile stands in when the wave
+            // has none): these loads sit between the chunk's first gathers
+            // and their use, and must not make the vmcnt count path-dependent.
+            const int te = min(t, ntiles - 1);
+            th = hdr[te];
             bt += th.z;
 #pragma unroll
             for (int p = 0; p < 3; ++p) bn[p] = bt[p * 64];
-            const int xb = 16 * t + (lane & 15);
-            if (xb < h.out_len) bias = tbias[xb];
+            const int xb = 16 * te + (lane & 15);
+            bias = tbias[min(xb, h.out_len - 1)];
+            if (!has_tile) th.y = 0;
         }
 
         // Phase 1: new M columns → planar LDS ring.  Three register sets
         // rotate so that each step's gathers have two steps of HSV work to land.
         const int c0 = ck.c0, ng4 = ck.ng4, nsteps = ck.nsteps;
-        auto process = [&](const Raw4& P, int st) {
+        // newer = gather loads issued after P's (4 per live later set)
+        auto process = [&](Raw4& P, int st, int newer) {
+            if (IPP_HP_ASMG) asm_wait(P.p, P.live ? newer : -1);
             // SQ8: after the quad transpose, lane i of quad h (= lane>>2 & 1)
             // owns row (lane>>3) + 8(i>>1), columns 8(i&1) + 4h .. +3 of the step
             const int qi = lane & 3;
-            const int cg = IPP_HP_SQ8 ? wave * 4 + 16 * st + 2 * (qi & 1) + ((lane >> 2) & 1)
-                                      : wave * 4 + 16 * st + (lane & 3);
+            // Q22: after the pair exchange lane dx holds columns 8gc + 4dx .. +3
+            const int cg = IPP_HP_SQ8   ? wave * 4 + 16 * st + 2 * (qi & 1) + ((lane >> 2) & 1)
+                           : IPP_HP_Q22 ? wave * 4 + 4 * HP_NW * st + 2 * ((lane >> 2) & 1) + (lane & 1)
+                                        : wave * 4 + 4 * HP_NW * st + (lane & 3);
             const int rw = IPP_HP_SQ8 ? (lane >> 3) + 8 * (qi >> 1) : r;
             const int x = c0 + 4 * cg;
             const bool active = (cg < ng4) && (rw < nrows);
@@ -315,7 +447,9 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                 zb[k] = ~0u;
                 if (ZONES) {
                     // column of instruction k's pixel (SQ8: before the transpose)
-                    const int xk = IPP_HP_SQ8 ? c0 + 16 * wave + 64 * st + (lane & 7) + 8 * (k & 1) : x + k;
+                    const int xk = IPP_HP_SQ8   ? c0 + 16 * wave + 64 * st + (lane & 7) + 8 * (k & 1)
+                                   : IPP_HP_Q22 ? c0 + 16 * wave + HP_STEPC * st + 8 * ((lane >> 2) & 1) + (lane & 1) + 2 * k
+                                                : x + k;
                     const uint32_t zr = IPP_HP_SQ8 ? ((k >> 1) ? (zrow >> 16) : (zrow & 0xFFFFu)) : zrow;
                     zb[k] = 0;
 #pragma unroll
@@ -334,11 +468,13 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                     px[k] = (DBG & 2) ? (raw | 0x80808080u) : hsv2_px<NR, ZONES>(T, raw, zb[k]);
                 }
                 if (IPP_HP_SQ8) quad_transpose4(px, lane);
+                if (IPP_HP_Q22) pair_regroup(px, lane & 1);
                 transpose4(px[0], px[1], px[2], px[3], ch);
             } else if (ZONES) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) px[k] = hsv2_px<NR, ZONES>(T, 0u, zb[k]);
                 if (IPP_HP_SQ8) quad_transpose4(px, lane);
+                if (IPP_HP_Q22) pair_regroup(px, lane & 1);
                 transpose4(px[0], px[1], px[2], px[3], ch);
             } else {
 #pragma unroll
@@ -350,48 +486,58 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                 for (int c = 0; c < 4; ++c) *reinterpret_cast<uint32_t*>(&win[c][rw][pos]) = ch[c];
             }
         };
-        auto iss = [&](int st2, Raw4& o) {
-            if (st2 < nsteps) issue(ck, st2, xxl + st2 * sx, yyl + st2 * sy, xl + 64 * st2, o);
-        };
+        auto iss = [&](int st2, Raw4& o) { issue(ck, st2, xxl + st2 * sx, yyl + st2 * sy, xl + HP_STEPC * st2, o); };
+        // The loops run whole register-set rotations (a trailing step past
+        // nsteps is dead: fill gathers, no ring writes).  With no early exit
+        // each set keeps its registers; an exit mid-rotation made the
+        // compiler shuffle the sets through copies, and copying a register
+        // whose load is in flight waits for that load.
+        static_assert(!(IPP_HP_ASMG && IPP_HP_DEPTH > 2), "IPP_HP_ASMG waits for depth 2");
         if (IPP_HP_DEPTH > 2) {  // four register sets: gathers three steps ahead
             for (int st = 0; st < nsteps; st += 4) {
                 iss(st + 3, RD);
-                process(RA, st);
-                if (st + 1 >= nsteps) break;
+                process(RA, st, 4 * (RB.live + RC.live + RD.live));
                 iss(st + 4, RA);
-                process(RB, st + 1);
-                if (st + 2 >= nsteps) break;
+                process(RB, st + 1, 4 * (RC.live + RD.live + RA.live));
                 iss(st + 5, RB);
-                process(RC, st + 2);
-                if (st + 3 >= nsteps) break;
+                process(RC, st + 2, 4 * (RD.live + RA.live + RB.live));
                 iss(st + 6, RC);
-                process(RD, st + 3);
+                process(RD, st + 3, 4 * (RA.live + RB.live + RC.live));
             }
         } else {
             for (int st = 0; st < nsteps; st += 3) {
                 iss(st + 2, RC);
-                process(RA, st);
-                if (st + 1 >= nsteps) break;
+                process(RA, st, 4 * (RB.live + RC.live));
                 iss(st + 3, RA);
-                process(RB, st + 1);
-                if (st + 2 >= nsteps) break;
+                process(RB, st + 1, 4 * (RC.live + RA.live));
                 iss(st + 4, RB);
-                process(RC, st + 2);
+                process(RC, st + 2, 4 * (RA.live + RB.live));
             }
         }
 
-        // Next chunk's first two steps: their gathers fly during phase 2.
+        // Next chunk's first steps.  IPP_HP_NEXT_EARLY: issued here, so they
+        // fly during phase 2 (whose K-step tap loads, issued after them, then
+        // wait for them too: vmcnt retires in order); else issued after phase 2.
         const int s1 = ck.s1;
         const bool more = s1 < ntiles;
-        if (more) {
-            ck = hp2_chunk(hdr, s1, ntiles, filled, wave);
-            xl = lane_x(ck);
-            xxl = rx0 + (uint32_t)xl * (uint32_t)B.b0;
-            yyl = ry0 + (uint32_t)xl * (uint32_t)B.b3;
-            if (ck.nsteps > 0) issue(ck, 0, xxl, yyl, xl, RA);
-            if (ck.nsteps > 1) issue(ck, 1, xxl + sx, yyl + sy, xl + 64, RB);
-            if (IPP_HP_DEPTH > 2 && ck.nsteps > 2) issue(ck, 2, xxl + 2 * sx, yyl + 2 * sy, xl + 128, RC);
-        }
+        auto next_chunk = [&]() {
+            if (more) {
+                ck = hp2_chunk(hdr, s1, ntiles, filled, wave);
+                xl = lane_x(ck);
+                xxl = rx0 + (uint32_t)xl * (uint32_t)B.b0;
+                yyl = ry0 + (uint32_t)xl * (uint32_t)B.b3;
+            } else {
+                ck.nsteps = 0;  // dead loads: the issue count stays path-independent
+            }
+            issue(ck, 0, xxl, yyl, xl, RA);
+            issue(ck, 1, xxl + sx, yyl + sy, xl + HP_STEPC, RB);
+            if (IPP_HP_DEPTH > 2) issue(ck, 2, xxl + 2 * sx, yyl + 2 * sy, xl + 2 * HP_STEPC, RC);
+        };
+        // The chunk's first tap and bias loads (issued before its gathers) are
+        // waited for here on every path: a compiler wait for them after the
+        // next chunk's asm gathers would drain those as well.
+        if (IPP_HP_ASMG) asm volatile("" ::"v"(bn[0].x), "v"(bn[1].x), "v"(bn[2].x), "v"(bias));
+        if (IPP_HP_NEXT_EARLY == 1) next_chunk();
         HP_STAMP(ts1);
         __syncthreads();
         HP_STAMP(ts2);
@@ -400,7 +546,52 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // columns of one channel (lane l: row l&15, bytes 16(l>>4)..+15),
         // B = 64 columns × 16 outputs of one tap byte plane.  D lane l =
         // output l&15, rows 4(l>>4)..+3 = exactly one 16-B T group.
-        if (has_tile) {
+        if (HP_NW == 8 && has_tile) {
+            // Two 4-row groups of this wave's row half; A row i of a group =
+            // (channel i >> 2, row i & 3), so D lane l holds channel l >> 4,
+            // rows 0..3 of the group for output l & 15: one dword of T.
+            const int hf = wave >> 2;
+            i32x4 acc[2][3];
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) acc[g][p] = i32x4{0, 0, 0, 0};
+            const int ach = (lane >> 2) & 3, arow = 8 * hf + (lane & 3), akoff = 16 * (lane >> 4);
+#pragma unroll 1
+            for (int ks = 0; ks < th.y; ++ks) {
+                i32x4 bq[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) bq[p] = __builtin_bit_cast(i32x4, bn[p]);
+                if (ks + 1 < th.y) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) bn[p] = bt[((ks + 1) * 3 + p) * 64];
+                }
+                const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    const i32x4 a = *reinterpret_cast<const i32x4*>(&win[ach][arow + 4 * g][pos]);
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        acc[g][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[p], acc[g][p], 0, 0, 0);
+                }
+            }
+            const int xo = 16 * t + (lane & 15);
+            if (xo < h.out_len) {
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    uint32_t o = 0u;
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int32_t ss = bias + acc[g][0][rr] + (acc[g][1][rr] << 8) + (acc[g][2][rr] << 16);
+                        o |= clip8(ss) << (8 * rr);
+                    }
+                    const int grp = (row0 >> 2) + 2 * hf + g;
+                    uint32_t* dst = reinterpret_cast<uint32_t*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) +
+                                    4 * xo + (lane >> 4);
+                    *dst = o ^ 0x80808080u;
+                }
+            }
+        } else if (HP_NW == 4 && has_tile) {
             i32x4 acc[4][3];
 #pragma unroll
             for (int c = 0; c < 4; ++c)
@@ -425,6 +616,9 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                         acc[c][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[p], acc[c][p], 0, 0, 0);
                 }
             }
+            // IPP_HP_NEXT_EARLY 2: after the last tap load, so no compiler wait
+            // on those drains the gathers
+            if (IPP_HP_NEXT_EARLY == 2) next_chunk();
             const int xo = 16 * t + (lane & 15);
             if (xo < h.out_len) {
                 uint32_t outc[4] = {0u, 0u, 0u, 0u};
@@ -441,12 +635,14 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                                   outc[3] ^ 0x80808080u);
             }
         }
+        if (IPP_HP_NEXT_EARLY == 2 && !(HP_NW == 4 && has_tile)) next_chunk();
         HP_STAMP(ts3);
         st_p1 += ts1 - ts0;
         st_b1 += ts2 - ts1;
         st_p2 += ts3 - ts2;
         ++st_n;
         if (!more) break;
+        if (IPP_HP_NEXT_EARLY == 0) next_chunk();
         __syncthreads();
         HP_STAMP(ts4);
         st_b2 += ts4 - ts3;
@@ -536,11 +732,12 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
 #define IPP_HP_BANDS 1
 #endif
 template <int NR, bool ZONES, int CN, int DBG = 0, bool COPY = false, int BANDS = IPP_HP_BANDS>
-__global__ void __launch_bounds__(256 * BANDS) __attribute__((amdgpu_waves_per_eu(IPP_HP_WAVES)))
+__global__ void __launch_bounds__(64 * HP_NW * BANDS) __attribute__((amdgpu_waves_per_eu(IPP_HP_WAVES)))
 k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
               const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp, const uint8_t* __restrict__ bg,
               uint8_t* __restrict__ dst, int cpi) {
     __shared__ Hpass2Lds<NR, BANDS> L;
+    static_assert(BANDS == 1 || HP_NW == 4, "bands per block assume 4 waves per band");
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     // tiles_y = H-pass blocks per item (BANDS bands each).  COPY: each item
     // owns tiles_y H-pass blocks followed by cpi background-copy blocks, so
@@ -549,14 +746,14 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
     const int im = b / per_item;
     const int tb = b - im * per_item;
     if (COPY && tb >= tiles_y) {
-        bg_copy_outside_bands<256 * BANDS>(descs[im].p, bg, dst, tb - tiles_y, cpi);
+        bg_copy_outside_bands<64 * HP_NW * BANDS>(descs[im].p, bg, dst, tb - tiles_y, cpi);
         return;
     }
     const ipp_gather_desc g = descs[im].g;
     const ipp_resample_desc h = descs[im].h;
     if (tb * BANDS * HR >= h.lines) return;  // block-uniform
     const int band = BANDS == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
-    const int wib = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);  // wave in the band
+    const int wib = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & (HP_NW - 1));  // wave in the band
     const int row0 = (tb * BANDS + band) * HR;
     const bool band_on = row0 < h.lines;  // idle bands keep to the block's barriers
 
@@ -567,7 +764,7 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
     int32_t zc0[ZONES ? NR : 1], zcw[ZONES ? NR : 1];
     uint32_t zrow = 0;
     const int lane = threadIdx.x & 63;
-    const int y = h.line0 + row0 + (lane >> 2);
+    const int y = h.line0 + row0 + (IPP_HP_Q22 ? 2 * (lane >> 3) + ((lane >> 1) & 1) : lane >> 2);
     if (ZONES) {
 #pragma unroll
         for (int k = 0; k < NR; ++k) {
@@ -596,6 +793,7 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
     const uint64_t sbu = reinterpret_cast<uint64_t>(S.base);
     Hp2Block B;
     B.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(sbu), (short)0, nrec, 0x00020000);
+    B.rsv = u32x4_t{(uint32_t)sbu, (uint32_t)(sbu >> 32) & 0xFFFFu, (uint32_t)nrec, 0x00020000u};
     B.lim = S.lim;
     B.rowx = (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1;
     B.rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
@@ -632,8 +830,9 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
         int blo = 0x3FFFFFFF, bhi = -0x3FFFFFFF;
 #pragma unroll
         for (int rr = 0; rr < HR; ++rr) {
-            blo = min(blo, __builtin_amdgcn_readlane(ilo, 4 * rr));
-            bhi = max(bhi, __builtin_amdgcn_readlane(ihi, 4 * rr));
+            const int lr = IPP_HP_Q22 ? 8 * (rr >> 1) + 2 * (rr & 1) : 4 * rr;  // a lane of row rr
+            blo = min(blo, __builtin_amdgcn_readlane(ilo, lr));
+            bhi = max(bhi, __builtin_amdgcn_readlane(ihi, lr));
         }
         B.xlo = (DBG & 8) ? -0x3FFFFFFF : blo;
         B.xhi = (DBG & 8) ? 0x3FFFFFFF : bhi;
@@ -792,7 +991,7 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
     if (bg && dst) {  // H pass + the background rows outside the overlay bands
         const int cpi = BANDS == 1 ? copy_blocks_per_item() : 1;
         const dim3 g2((uint32_t)(n * (tyb + cpi)));
-        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 0, true>), g2, dim3(256 * BANDS), 0, s, src, tmp, coefs, descs,
+        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, 0, true>), g2, dim3(64 * HP_NW * BANDS), 0, s, src, tmp, coefs, descs,
                            tyb, hp, bg, dst, cpi);
         return;
     }
@@ -804,7 +1003,7 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
     if (dbg >= 10 && NR == 4 && !ZONES && CN == 3) {
         switch (dbg - 10) {
 #define IPP_DIAG_CASE(D) \
-    case D: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, D, false, 1>), grid, dim3(256), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); return;
+    case D: hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, D, false, 1>), grid, dim3(64 * HP_NW), 0, s, src, tmp, coefs, descs, ty, hp, bg, dst, 0); return;
             IPP_DIAG_CASE(1) IPP_DIAG_CASE(2) IPP_DIAG_CASE(3) IPP_DIAG_CASE(4) IPP_DIAG_CASE(5) IPP_DIAG_CASE(6)
             IPP_DIAG_CASE(7) IPP_DIAG_CASE(8) IPP_DIAG_CASE(16) IPP_DIAG_CASE(20)
 #undef IPP_DIAG_CASE
@@ -812,7 +1011,7 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
         }
     }
 #endif
-    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), dim3((uint32_t)(n * tyb)), dim3(256 * BANDS), 0, s, src, tmp,
+    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), dim3((uint32_t)(n * tyb)), dim3(64 * HP_NW * BANDS), 0, s, src, tmp,
                        coefs, descs, tyb, hp, bg, dst, 0);
 }
 

@@ -1,0 +1,8 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for v in asmg asmgq asmgqe; do
+  IPP_LIB_PATH=$PWD/variants/$v/libipp.so timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -k "pipe" -x -q --timeout 180 --timeout-method thread > gpurun_out/pt_$v.log 2>&1 || { tail -30 gpurun_out/pt_$v.log; exit 21; }
+  echo "$v $(tail -1 gpurun_out/pt_$v.log)"
+done
+bash tools/ab.sh "" old q22 asmg asmgq asmgqe old q22 asmg asmgq asmgqe || exit 20
