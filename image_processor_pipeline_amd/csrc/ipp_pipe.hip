@@ -139,9 +139,12 @@ struct Hp2Block {
 };
 
 // 4 gathered pixels of lane group x .. x+3 (raw dwords; 0 outside the window).
+// CLAMP: only the image's last pixel can have its dword cross the image end
+// (bytes beyond it are out of range and would zero the whole dword); that
+// pixel is loaded one byte early and shifted down, marked by bit 1 + k of fl.
 struct Raw4 {
     uint32_t p[4];
-    uint32_t sh[4];
+    uint32_t fl;  // CLAMP: bit 1 + k = pixel k was loaded one byte early
     bool any;
     bool live;  // IPP_HP_ASMG: the step's loads were issued (block-uniform)
 };
@@ -197,6 +200,7 @@ template <int CN, bool CLAMP, int DBG = 0, int XSTEP = 1>
 __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32_t yy, int x, bool live, Raw4& o) {
     bool any = false;
     uint32_t off[4];
+    if (CLAMP) o.fl = 0u;
     if (live) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -205,7 +209,7 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
             uint32_t o1 = (uint32_t)__mul24(yin, B.pitch) + (uint32_t)__umul24((uint32_t)xin, (uint32_t)CN);
             if (CLAMP) {
                 const uint32_t offc = min(o1, B.lim);
-                o.sh[k] = ok ? (o1 - offc) << 3 : 0u;
+                o.fl |= (uint32_t)(o1 != offc) << (1 + k);
                 o1 = offc;
             }
             if (DBG & 1) o1 = (uint32_t)((x >> 6) * 768 + (threadIdx.x & 63) * 3 + k * 192 + (threadIdx.x >> 8) * 3072);
@@ -217,10 +221,7 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            off[k] = 0xFFFFFFFFu;
-            if (CLAMP) o.sh[k] = 0u;
-        }
+        for (int k = 0; k < 4; ++k) off[k] = 0xFFFFFFFFu;
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -238,6 +239,7 @@ template <int CN, bool CLAMP>
 __device__ __forceinline__ void hp2_issue_sq8(const Hp2Block& B, uint32_t xx, uint32_t yy, bool live, Raw4& o) {
     bool any = false;
     uint32_t off[4];
+    if (CLAMP) o.fl = 0u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t xk = xx + (k & 1) * 8u * (uint32_t)B.b0 + (k >> 1) * (uint32_t)B.b1x8;
@@ -247,7 +249,7 @@ __device__ __forceinline__ void hp2_issue_sq8(const Hp2Block& B, uint32_t xx, ui
         uint32_t o1 = (uint32_t)__mul24(yin, B.pitch) + (uint32_t)__umul24((uint32_t)xin, (uint32_t)CN);
         if (CLAMP) {
             const uint32_t offc = min(o1, B.lim);
-            o.sh[k] = ok ? (o1 - offc) << 3 : 0u;
+            o.fl |= (uint32_t)(o1 != offc) << (1 + k);
             o1 = offc;
         }
         off[k] = ok ? o1 : 0xFFFFFFFFu;
@@ -280,7 +282,9 @@ __device__ __forceinline__ void hp2_issue_sq8(const Hp2Block& B, uint32_t xx, ui
 #define IPP_HP_LIVESKIP 1
 #endif
 // Next chunk's first gathers: 0 after phase 2, 1 before it (before the
-// barrier), 2 after its MFMAs (before the T store).
+// barrier).  (Issuing them after the MFMAs, before the T store, broke parity:
+// with the accumulators live the compiler moved the in-flight gather
+// registers — the hazard IPP_HP_ASMG relies on the parity tests to catch.)
 #ifndef IPP_HP_NEXT_EARLY
 #define IPP_HP_NEXT_EARLY 1
 #endif
@@ -374,10 +378,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     uint32_t xxl = rx0 + (uint32_t)xl * (uint32_t)B.b0, yyl = ry0 + (uint32_t)xl * (uint32_t)B.b3;
     Raw4 RA, RB, RC, RD;
     RA.live = RB.live = RC.live = RD.live = false;
-    if (CLAMP) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) RA.sh[k] = RB.sh[k] = RC.sh[k] = RD.sh[k] = 0u;
-    }
+    RA.fl = RB.fl = RC.fl = RD.fl = 0u;
     // A step = 16 columns of 16 rows per wave; steps wholly outside the band's
     // valid columns are all fill: no gathers, no HSV, constant window bytes.
     auto step_live = [&](const Hp2Chunk& c, int st) {
@@ -464,7 +465,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     uint32_t raw = P.p[k];
-                    if (CLAMP) raw >>= P.sh[k];
+                    if (CLAMP) raw >>= ((P.fl >> (1 + k)) & 1u) << 3;
                     px[k] = (DBG & 2) ? (raw | 0x80808080u) : hsv2_px<NR, ZONES>(T, raw, zb[k]);
                 }
                 if (IPP_HP_SQ8) quad_transpose4(px, lane);
@@ -616,9 +617,6 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                         acc[c][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[p], acc[c][p], 0, 0, 0);
                 }
             }
-            // IPP_HP_NEXT_EARLY 2: after the last tap load, so no compiler wait
-            // on those drains the gathers
-            if (IPP_HP_NEXT_EARLY == 2) next_chunk();
             const int xo = 16 * t + (lane & 15);
             if (xo < h.out_len) {
                 uint32_t outc[4] = {0u, 0u, 0u, 0u};
@@ -635,7 +633,6 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                                   outc[3] ^ 0x80808080u);
             }
         }
-        if (IPP_HP_NEXT_EARLY == 2 && !(HP_NW == 4 && has_tile)) next_chunk();
         HP_STAMP(ts3);
         st_p1 += ts1 - ts0;
         st_b1 += ts2 - ts1;
