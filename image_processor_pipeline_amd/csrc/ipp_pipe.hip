@@ -271,7 +271,9 @@ __device__ __forceinline__ void hp2_issue_sq8(const Hp2Block& B, uint32_t xx, ui
 // A lane-pair exchange afterwards gives each lane 4 consecutive columns of
 // its row again.  Measured on the box: 1.7 % faster than map 0, although the
 // L1 tag lookups per gather instruction rose from 65 to 76
-// (TCP_TOTAL_CACHE_ACCESSES / TA_BUFFER_READ_WAVEFRONTS).
+// (TCP_TOTAL_CACHE_ACCESSES / TA_BUFFER_READ_WAVEFRONTS); with the asm waits
+// 9.25 ms against 10.02 (map 0) and 9.72 (a 4×4 block per 16-lane group and a
+// DPP quad transpose afterwards: 66 lookups per instruction).
 #ifndef IPP_HP_Q22
 #define IPP_HP_Q22 1
 #endif
@@ -288,6 +290,7 @@ __device__ __forceinline__ void hp2_issue_sq8(const Hp2Block& B, uint32_t xx, ui
 #ifndef IPP_HP_NEXT_EARLY
 #define IPP_HP_NEXT_EARLY 1
 #endif
+// (depth 3 with the asm waits: 9.77 vs 9.02 ms, 2 VGPRs of spills)
 #ifndef IPP_HP_DEPTH  // phase-1 gather depth: steps in flight ahead of the one processed
 #define IPP_HP_DEPTH 2
 #endif
