@@ -278,6 +278,27 @@ def test_pipe_crop_reaching_source_end(D):
             assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (margins, i)
 
 
+def test_pipe_random_geometry_stress(D):
+    """Many small items of random shapes, margins (zero margins included:
+    the CLAMP path), angles and overlay ratios.  The H pass issues its source
+    gathers by inline asm with hand-placed vmcnt waits (gather
+    waits); a compiler copy of a register whose gather is still in flight would
+    read stale bytes, which bit-exact comparisons on varied geometry expose."""
+    from image_processor_pipeline_amd import fused
+    rng = np.random.default_rng(77)
+    for trial in range(6):
+        H, W = int(rng.integers(40, 200)), int(rng.integers(40, 200))
+        bh, bw = int(rng.integers(64, 160)), int(rng.integers(64, 160))
+        m = [int(v) for v in rng.integers(0, 6, 4)]
+        if trial % 2 == 0:
+            m[1], m[3] = 0, 0
+        cfg = fused.PipeConfig(margins=tuple(m), scale_min=0.3, scale_max=0.8)
+        src, bgs, plan, got = _run_pipe(8, H, W, 2, bh, bw, cfg, seed=100 + trial)
+        for i in range(len(got)):
+            exp = opipe.pipe_item(src[i], bgs, plan.params[i], cfg)
+            assert np.array_equal(got[i], exp), (trial, H, W, m, i, plan.params[i])
+
+
 def test_pipe_edge_parameters_vs_oracle(D):
     """Explicit item parameters at the edges of their ranges: Pillow's
     right-angle fast paths (0/90/180/270 and their wraps) under every flip,
