@@ -404,8 +404,14 @@ __device__ __forceinline__ void tile_words(const uint8_t* __restrict__ img, cons
 }
 
 // K1: one wave per 64×64 tile, WAVES tiles side by side per block.
+#ifndef IPP_CCL_WPE  // K1 occupancy target (waves per SIMD; 0 = the compiler's choice): 6 → 49-55 VGPRs, 7 waves/SIMD, no spills; 3.44 vs 3.63 ms per video4k step (the default choice was 85-89 VGPRs, 5 waves)
+#define IPP_CCL_WPE 6
+#endif
 template <int SRC, int NR, bool ZONES>
 __global__ void __launch_bounds__(64 * WAVES)
+#if IPP_CCL_WPE
+__attribute__((amdgpu_waves_per_eu(IPP_CCL_WPE)))
+#endif
 k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
             const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, int32_t* __restrict__ counts,
             int groups_per_img, int groups_x, ipp_hsv_params hp) {
