@@ -15,7 +15,12 @@ LIB := $(PKG)/libipp.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 HOSTFLAGS := -O2 -std=c++17 -fPIC -Iinclude
 
-all: $(LIB)
+all: $(LIB) $(OBJDIR)/ipp_pipe.s
+
+# The H pass's ISA, for the static check of its hand-waited gathers
+# (tools/asm_hazard.py, tests/test_asm_gather_hazard.py).
+$(OBJDIR)/ipp_pipe.s: $(CSRC)/ipp_pipe.hip $(HDRS) | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -S --cuda-device-only $< -o $@
 
 # Pillow's BILINEAR (double) and Blend (float) arithmetic is plain mul/add
 # (x86-64 baseline, no FMA): these files must not contract a*b+c into fma,

@@ -29,11 +29,12 @@
 
 namespace {
 
-constexpr int HR = 16;            // H-pass rows per block (one 16-row band)
+constexpr int HR = 16;            // H-pass rows per block (4 per thread)
 constexpr int RING = 512;         // window ring: M columns x live at x & (RING - 1)
 // LDS bytes per plane row of the window ring.  544 ≡ 8 dwords mod 64 banks:
 // the phase-2 ds_read_b128 (4 lane groups of 16, 4 dwords each) then covers
-// 64 distinct banks per group (MI355X_MICROARCH.md §LDS).
+// 64 distinct banks per group, and the phase-1 ds_write_b32 rows pair up 2-way,
+// which a dword store absorbs (MI355X_MICROARCH.md §LDS).
 constexpr int WSTRIDE = 544;
 // ipp_pipe_hpass_bgcopy: background-copy blocks per item.  Diagnostic builds
 // (-DIPP_DIAG) may override it through the environment; the product build
@@ -68,61 +69,52 @@ __device__ __forceinline__ void transpose4(uint32_t p0, uint32_t p1, uint32_t p2
     ch[3] = perm(hi23, hi01, 0x07060302u);
 }
 
+// Q22 lane pair (dx = lane & 1) holding columns {dx, dx + 2, dx + 4, dx + 6}
+// of one row → lane 0 holds columns 0..3, lane 1 columns 4..7 (two DPP
+// swaps with the partner lane).
+__device__ __forceinline__ void pair_regroup(uint32_t (&a)[4], bool o1) {
+    const uint32_t s0 = o1 ? a[0] : a[2], s1 = o1 ? a[1] : a[3];
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s0, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0xB1, 0xF, 0xF, false);
+    const uint32_t b0 = o1 ? r0 : a[0], b1 = o1 ? a[2] : r0, b2 = o1 ? r1 : a[1], b3 = o1 ? a[3] : r1;
+    a[0] = b0;
+    a[1] = b1;
+    a[2] = b2;
+    a[3] = b3;
+}
+
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
-// H pass (MFMA taps) over LDS-staged source spans.
+// H pass (MFMA taps): per-pixel buffer-load gathers, table-driven HSV test.
 //
-// Block = one 16-row band of M (the rotated / flipped / cropped cut-out) of
-// one item, 4 waves.  It sweeps the band's M columns in chunks of ≤ 4 output
-// tiles whose input window fits the 512-column channel-planar LDS ring; phase
-// 2 of a chunk runs the LANCZOS taps on the matrix cores (below).
+// The M pixel is (R, G, B) of the source or black outside it (rotations.py
+// fills with transparent black and filtres_liste.py:84 reads the file back
+// with cv2.imread, which drops alpha, so fill and real black pixels are
+// indistinguishable from the HSV step on).  Hence:
+//   * gathers go through a buffer resource whose range check returns 0 for the
+//     out-of-window offset 0xFFFFFFFF — no validity bits, no value masking;
+//   * the inRange union is decided by three LDS mask tables instead of packed
+//     compares: bit k of vm[v], sm[s], hm[h + 32] says range k holds on that
+//     channel, so  excluded ⟺ vm[v] & sm[s] & hm[h + 32] (& zone bits) ≠ 0.
 //
-// The ring's new columns arrive in "pieces" of C ≤ 128 M columns.  A piece's
-// 16 × C M pixels come from a parallelogram of the source (NEAREST rotation,
-// rotations.py:96).  For each source row j crossing it, the exact column span
-// [x_lo(j), x_hi(j)] is computed from the parallelogram's edges (float, with
-// 1/64 px of slack, so a superset of the pixels the 16.16 gather can hit), and
-// the block loads those spans with 12-byte (4-pixel) coalesced buffer loads —
-// one TA wavefront per 256 source pixels instead of one per 64 gathered M
-// pixels.  Each 4-pixel group goes through the table-driven HSV test
-// (filtres_liste.py:84-134) right after its load, densely, and lands in the
-// stage as 4 window bytes per pixel.  The M pixels then read their source
-// pixel from the stage (two ds_read_b32: the row's base, the pixel) and write
-// the ring.  No gather goes through the texture path any more.
-//
-// Source row j of a piece is staged at slots [j·S, j·S + cnt(j)) (16 B each,
-// S = a per-block bound on the groups per row, so no prefix sum is needed):
-//   rowtab[j] = 16 (j S - x_lo(j)/4),   pixel x of row j at rowtab[j] + 4 x.
-//
-// Pieces are software-pipelined across two barriers per piece:
-//   A: issue the loads of piece q+1, the spans of piece q+2, gather piece q
-//      from the stage into the ring;
-//   B: HSV + stage writes of piece q+1; phase 2 when q ends its chunk.
+// Block = one 16-row band of one item, 4 waves.  It sweeps the item's output
+// tiles in chunks of ≤ 4 tiles whose input window fits the 512-column
+// channel-planar LDS ring.  Phase 1 gathers the chunk's new M columns into
+// the ring (16 columns × 16 rows per wave and step; a lane quad takes a 2×2
+// block of M pixels, whose source pixels lie within ~1.5 px of each other);
+// phase 2 runs the taps on the matrix cores.
+// (An LDS-staged form — coalesced source spans, dense HSV — was bit-exact but
+// 1.6× slower, VALU-bound: DESIGN.md §3, profiles/r03_staged/.)
 // ---------------------------------------------------------------------------
-constexpr int HP_THREADS = 256;     // 4 waves, one 16-row band
-constexpr int HP_SLOTS = 896;       // stage slots (4 source pixels, 16 B each)
-constexpr int HP_MAXROWS = 160;     // staged source rows per piece
-constexpr int HP_CMAX = 128;        // M columns per piece (at most)
-constexpr float HP_EPS = 1.0f / 64.0f;  // px slack of the span arithmetic (float error < 1e-2 px)
-
 typedef uint8_t WinRing[4][HR][WSTRIDE];   // planar window ring, bytes p ^ 0x80
 
 template <int NR>
-struct __attribute__((aligned(16))) Hpass3Lds {
+struct __attribute__((aligned(16))) Hpass2Lds {
     WinRing win;
-    uint32_t stage[4 * (HP_SLOTS + 1)];   // staged pixels; the last slot holds the fill pixel
-    int32_t rowinfo[2][HP_MAXROWS];       // per staged row (piece parity): x_lo/4 | cnt << 16
-    int32_t rowtab[HP_MAXROWS];           // per staged row: stage byte offset of source column 0
-    HsvTables<NR> T;                      // table-driven HSV test (ipp_hsv.h)
-};
-
-// What a stage pixel holds.  0: the final window byte quad (no zones);
-// 1: RGB | range bits << 24 (zones, ≤ 8 ranges: the zone test needs the M
-// position); 2: raw RGB (zones, > 8 ranges: the HSV test runs after the gather).
-template <int NR, bool ZONES>
-struct StageMode {
-    static constexpr int v = !ZONES ? 0 : (NR <= 8 ? 1 : 2);
+    HsvTables<NR> T;               // table-driven HSV test (ipp_hsv.h)
+    int32_t zc[NR > 8 ? 2 * NR : 1];  // > 8 ranges with zones: column bounds here, not in registers
 };
 
 // M pixel → window byte quad (p | α 255) ^ 0x80 when kept, 0x80808080 (transparent black) when excluded.
@@ -134,397 +126,116 @@ __device__ __forceinline__ uint32_t hsv2_px(const HsvTables<NR>& T, uint32_t raw
     return ex ? 0x80808080u : t;
 }
 
-// Diagnostic builds only (-DIPP_DIAG, wrong output): IPP_HP_X bit 0 = no
-// HSV in the stage, bit 1 = no gather, bit 2 = no phase 2, bit 3 = no loads.
-#if defined(IPP_DIAG) && defined(IPP_HP_X)
-constexpr int kHpX = IPP_HP_X;
-#else
-constexpr int kHpX = 0;
-#endif
-
-template <int NR, int MODE>
-__device__ __forceinline__ uint32_t stage_px(const HsvTables<NR>& T, uint32_t raw) {
-    if (MODE == 2) return raw;
-    if (kHpX & 1) return (raw | 0xFF000000u) ^ 0x80808080u;
-    const uint32_t ex = hsv_tab_excl<NR, false>(T, raw);
-    if (MODE == 1) return (raw & 0xFFFFFFu) | (ex << 24);
-    return ex ? 0x80808080u : (raw | 0xFF000000u) ^ 0x80808080u;
-}
-
-template <int NR, int MODE>
-__device__ __forceinline__ uint32_t window_px(const HsvTables<NR>& T, uint32_t v, uint32_t zb) {
-    if (MODE == 0) return v;
-    if (MODE == 1) return ((v >> 24) & zb) ? 0x80808080u : (v | 0xFF000000u) ^ 0x80808080u;
-    return hsv2_px<NR, true>(T, v, zb);
-}
-
 // Per-block state.
-struct Hp3Block {
-    __amdgpu_buffer_rsrc_t rs;   // source window, records = bytes to the image end
-    int32_t nrec;
-    uint32_t rowx0, rowy0;       // 16.16 source position of M column 0 of the band's row 0
-    int32_t b0, b1, b3, b4;      // 16.16 steps per M column (b0, b3) and per M row (b1, b4)
-    int32_t pitch, in_w, in_h;
-    int32_t xlo, xhi;            // the band's valid M columns ⊆ [xlo, xhi] (conservative)
-    int32_t C, lgcg;             // M columns per piece, log2(C / 4)
-    int32_t slots, spx;          // stage slots per staged row, bound on x_hi - x_lo
-    float rslots;                // 1 / slots
-    bool useV, useU;             // edge pairs usable as x(y) lines (|slope| ≤ 64)
-    bool bad;                    // no stage layout fits: nothing is staged (status bit 1)
+struct Hp2Block {
+    u32x4_t rsv;                // source window buffer resource (records = bytes to the image end)
+    uint32_t lim;               // CLAMP: last byte offset where a dword fits
+    uint32_t rowx, rowy;        // 16.16 source position of column 0 of the lane's row
+    int32_t b0, b3, pitch, in_w, in_h;
+    int32_t xlo, xhi;           // band's valid M columns ⊆ [xlo, xhi] (conservative)
 };
 
-// Bound on a slab's x extent (px) for a parallelogram with sides U (16 M
-// rows) and V (a piece's columns), the same formula for the block's bound and
-// for every piece: the polygon's x extent, or with both edge pairs usable the
-// longest horizontal chord plus the boundary's x drift over a slab of
-// height 1 + 2 eps.
-__device__ __forceinline__ float hp3_extent(float ux, float uy, float vx, float vy, bool useV, bool useU) {
-    float ext = fabsf(vx) + fabsf(ux);
-    if (useV && useU) {
-        const float chord = fabsf(ux * vy - uy * vx) * __builtin_amdgcn_rcpf(fmaxf(fabsf(vy), fabsf(uy)));
-        const float slope = fmaxf(fabsf(vx * __builtin_amdgcn_rcpf(vy)), fabsf(ux * __builtin_amdgcn_rcpf(uy)));
-        ext = fminf(ext, chord * (1.0f + 1e-5f) + 2.0f * (1.0f + 2.0f * HP_EPS) * slope * (1.0f + 1e-5f));
-    }
-    return ext;
+// 4 gathered pixels of a lane (raw dwords; 0 outside the window).  CLAMP:
+// only the image's last pixel can have its dword cross the image end (bytes
+// beyond it are out of range and would zero the whole dword); that pixel is
+// loaded one byte early and shifted down, marked by bit 1 + k of fl.
+struct Raw4 {
+    uint32_t p[4];
+    uint32_t fl;  // CLAMP: bit 1 + k = pixel k was loaded one byte early
+    bool any;     // some pixel of the lane is inside the window
+    bool live;    // the step's loads were issued (block-uniform)
+};
+
+// The gathers are issued by inline asm and waited for by hand.  The compiler
+// then neither counts them (its vmcnt bookkeeping merges paths pessimistically,
+// so a step skipped on some path made every later wait drain the gathers
+// issued for the steps ahead) nor copies their registers (a copy of a register
+// whose load is in flight would wait for it — or, worse, read it early: the
+// hazard tests/test_asm_gather_hazard.py checks in the emitted ISA).  Dead
+// steps issue nothing; a set is waited for with vmcnt(4 × live sets issued
+// after it), which never exceeds the loads really issued after it
+// (compiler-issued loads in between only make the wait stricter).  The wait
+// names the four data registers as in/out operands, so no use of them can
+// move above it.
+__device__ __forceinline__ uint32_t asm_gather(u32x4_t rs, uint32_t off) {
+    uint32_t v;
+    asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(rs));
+    return v;
+}
+// One asm statement on every path (newer = 8, 4, 0, or -1: the set was not
+// issued, no wait): with a wait per path the compiler merged the paths through
+// register copies, which read the data registers before their loads landed.
+// (The leading comment names the four registers in the emitted ISA, for the
+// static check in tools/asm_hazard.py.)
+__device__ __forceinline__ void asm_wait(uint32_t (&p)[4], int32_t newer) {
+    asm volatile(
+        "; gather wait %0 %1 %2 %3\n\t"
+        "s_cmp_eq_u32 %4, 8\n\t"
+        "s_cbranch_scc0 1f\n\t"
+        "s_waitcnt vmcnt(8)\n\t"
+        "s_branch 4f\n"
+        "1:\n\t"
+        "s_cmp_eq_u32 %4, 4\n\t"
+        "s_cbranch_scc0 2f\n\t"
+        "s_waitcnt vmcnt(4)\n\t"
+        "s_branch 4f\n"
+        "2:\n\t"
+        "s_cmp_eq_u32 %4, 0\n\t"
+        "s_cbranch_scc0 4f\n\t"
+        "s_waitcnt vmcnt(0)\n"
+        "4:"
+        : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3])
+        : "s"(newer)
+        : "scc");
 }
 
-// Piece width and stage layout for the block: the widest C ∈ {128, 64, 32,
-// 16} whose worst-case piece fits the stage.  0 when none does (the affine is
-// not a rotation; the pipe plans only rotations).
-__device__ __forceinline__ void hp3_layout(Hp3Block& B) {
-    const float k16 = 1.0f / 65536.0f;
-    B.useV = 64ll * llabs((long long)B.b3) > llabs((long long)B.b0);
-    B.useU = 64ll * llabs((long long)B.b4) > llabs((long long)B.b1);
-    const float ux = (float)(HR - 1) * (float)B.b1 * k16, uy = (float)(HR - 1) * (float)B.b4 * k16;
-    B.C = 0;
-    B.lgcg = 2;
-    B.slots = 1;
-    B.spx = 0;
-    B.rslots = 1.0f;
-    for (int C = HP_CMAX, lg = 5; C >= 16; C >>= 1, --lg) {
-        const float vx = (float)(C - 1) * (float)B.b0 * k16, vy = (float)(C - 1) * (float)B.b3 * k16;
-        const int rows = (int)(fabsf(vy) + fabsf(uy) + 4.0f * HP_EPS) + 2;
-        const int spx = (int)(hp3_extent(ux, uy, vx, vy, B.useV, B.useU) + 4.0f * HP_EPS) + 1;
-        const int slots = (spx + 3) / 4 + 1;
-        if (rows <= HP_MAXROWS && rows * slots <= HP_SLOTS) {
-            B.C = C;
-            B.lgcg = lg;
-            B.slots = slots;
-            B.spx = spx;
-            B.rslots = __builtin_amdgcn_rcpf((float)slots);
-            return;
+// Gathers of one live step: xx/yy = 16.16 source position of the lane's
+// first pixel (its next three are 2 columns apart).  Out-of-window pixels load
+// offset 0xFFFFFFFF (the range check returns 0).
+template <int CN, bool CLAMP>
+__device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32_t yy, Raw4& o) {
+    bool any = false;
+    uint32_t off[4];
+    if (CLAMP) o.fl = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int xin = (int32_t)xx >> 16, yin = (int32_t)yy >> 16;
+        const bool ok = ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h);
+        uint32_t o1 = (uint32_t)__mul24(yin, B.pitch) + (uint32_t)__umul24((uint32_t)xin, (uint32_t)CN);
+        if (CLAMP) {
+            const uint32_t offc = min(o1, B.lim);
+            o.fl |= (uint32_t)(o1 != offc) << (1 + k);
+            o1 = offc;
         }
+        off[k] = ok ? o1 : 0xFFFFFFFFu;
+        any |= ok;
+        xx += (uint32_t)(2 * B.b0);
+        yy += (uint32_t)(2 * B.b3);
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o.p[k] = asm_gather(B.rsv, off[k]);
+    o.any = any;
+    o.live = true;
 }
 
-struct Hp3Piece {
-    int xa, xb;        // M columns [xa, xb) written to the ring
-    int s0, s1;        // the chunk's output tiles [s0, s1)
-    int last;          // the chunk's last piece: phase 2 follows
-    int jlo, rows;     // staged source rows [jlo, jlo + rows); 0: nothing staged
-};
+constexpr int HP_NW = 4;              // waves per block (one 16-row band)
+constexpr int HP_STEPC = 16 * HP_NW;  // M columns per block-wide phase-1 step
 
 // Sticky status of the pipe kernels (ipp_pipe_status): bit 0 = an H-pass
 // output tile's input window was wider than the LDS ring (the plan violated
-// the ring limit of ipp.h; that tile's T columns are wrong); bit 1 = a band's
-// rotation did not fit the source stage (not a rotation, or a source wider
-// than 32767 px; its T rows are wrong).
+// the ring limit of ipp.h; that tile's T columns are wrong).
 __device__ int32_t g_pipe_status;
 
-// Spans of the piece's source rows → rowinfo (one row per thread).  ga..gb:
-// the piece's columns that can hold valid pixels.
-__device__ __forceinline__ void hp3_spans(const Hp3Block& B, int ga, int gb, int32_t* __restrict__ rowinfo,
-                                          Hp3Piece& pc) {
-    pc.jlo = 0;
-    pc.rows = 0;
-    if (ga >= gb || B.bad) return;
-    const float k16 = 1.0f / 65536.0f;
-    const float ax = (float)(int32_t)(B.rowx0 + (uint32_t)ga * (uint32_t)B.b0) * k16;
-    const float ay = (float)(int32_t)(B.rowy0 + (uint32_t)ga * (uint32_t)B.b3) * k16;
-    const float ux = (float)(HR - 1) * (float)B.b1 * k16, uy = (float)(HR - 1) * (float)B.b4 * k16;
-    const float vx = (float)(gb - 1 - ga) * (float)B.b0 * k16, vy = (float)(gb - 1 - ga) * (float)B.b3 * k16;
-    // vertices A = a, Bv = a + V, Cv = a + U + V, D = a + U
-    const float bx = ax + vx, by = ay + vy, cx = bx + ux, cy = by + uy, dx = ax + ux, dy = ay + uy;
-    const float xmin = fminf(fminf(ax, bx), fminf(cx, dx)), xmax = fmaxf(fmaxf(ax, bx), fmaxf(cx, dx));
-    const float ymin = fminf(fminf(ay, by), fminf(cy, dy)), ymax = fmaxf(fmaxf(ay, by), fmaxf(cy, dy));
-    const int jlo = max(0, (int)floorf(fmaxf(ymin - HP_EPS, -1.0f)));
-    const int jhi = min(B.in_h - 1, (int)floorf(fminf(ymax + HP_EPS, (float)B.in_h)));
-    const int rows = __builtin_amdgcn_readfirstlane(jhi - jlo + 1);
-    if (rows <= 0) return;
-    if (rows > HP_MAXROWS) {  // cannot happen under the block's layout bound
-        if (threadIdx.x == 0) atomicOr(&g_pipe_status, 2);
-        return;
-    }
-    pc.jlo = __builtin_amdgcn_readfirstlane(jlo);
-    pc.rows = rows;
-    if ((int)threadIdx.x >= rows) return;
-    // leftmost / rightmost vertex
-    float lx = ax, ly = ay, rx = ax, ry = ay;
-    if (bx < lx) { lx = bx; ly = by; }
-    if (cx < lx) { lx = cx; ly = cy; }
-    if (dx < lx) { lx = dx; ly = dy; }
-    if (bx > rx) { rx = bx; ry = by; }
-    if (cx > rx) { rx = cx; ry = cy; }
-    if (dx > rx) { rx = dx; ry = dy; }
-    // Boundary lines x = px + b (y - py).  V edges run through A and D, U
-    // edges through A and Bv; the V edge through A bounds the left side iff
-    // cross(U, V)·vy > 0, the U edge through A iff cross(U, V)·uy < 0.
-    // Near-horizontal edges (|slope| > 64) are dropped: fewer constraints only
-    // widen the spans, and they would amplify float error.
-    const float cr = ux * vy - uy * vx;
-    float l1x = xmin, l1y = 0.0f, l1b = 0.0f, r1x = xmax, r1y = 0.0f, r1b = 0.0f;
-    float l2x = xmin, l2y = 0.0f, l2b = 0.0f, r2x = xmax, r2y = 0.0f, r2b = 0.0f;
-    if (B.useV) {
-        const float bv = vx * __builtin_amdgcn_rcpf(vy);
-        const bool aL = cr * vy > 0.0f;
-        l1x = aL ? ax : dx; l1y = aL ? ay : dy; l1b = bv;
-        r1x = aL ? dx : ax; r1y = aL ? dy : ay; r1b = bv;
-    }
-    if (B.useU) {
-        const float bu = ux * __builtin_amdgcn_rcpf(uy);
-        const bool aL = cr * uy < 0.0f;
-        l2x = aL ? ax : bx; l2y = aL ? ay : by; l2b = bu;
-        r2x = aL ? bx : ax; r2y = aL ? by : ay; r2b = bu;
-    }
-    if (B.useV && !B.useU) { l2x = l1x; l2y = l1y; l2b = l1b; r2x = r1x; r2y = r1y; r2b = r1b; }
-    if (B.useU && !B.useV) { l1x = l2x; l1y = l2y; l1b = l2b; r1x = r2x; r1y = r2y; r1b = r2b; }
-    const int t = threadIdx.x;
-    const float j = (float)(jlo + t);
-    const float yl = fmaxf(j - HP_EPS, ymin), yh = fminf(j + 1.0f + HP_EPS, ymax);
-    // left boundary max(L1, L2) is convex in y: its minimum over the slab is at
-    // an end or at the leftmost vertex; the right boundary likewise
-    float xl = fminf(fmaxf(l1x + l1b * (yl - l1y), l2x + l2b * (yl - l2y)),
-                     fmaxf(l1x + l1b * (yh - l1y), l2x + l2b * (yh - l2y)));
-    float xr = fmaxf(fminf(r1x + r1b * (yl - r1y), r2x + r2b * (yl - r2y)),
-                     fminf(r1x + r1b * (yh - r1y), r2x + r2b * (yh - r2y)));
-    if (ly >= yl && ly <= yh) xl = lx;
-    if (ry >= yl && ry <= yh) xr = rx;
-    xl = fmaxf(xl, xmin);
-    xr = fminf(xr, xmax);
-    const int x_lo = max(0, (int)floorf(fmaxf(xl - HP_EPS, -1.0f)));
-    int x_hi = min(B.in_w - 1, (int)floorf(fminf(xr + HP_EPS, (float)B.in_w)));
-    if (x_hi - x_lo > B.spx) {  // cannot happen under the block's layout bound
-        atomicOr(&g_pipe_status, 2);
-        x_hi = x_lo + B.spx;
-    }
-    const int gl = x_lo >> 2;
-    const int cnt = x_lo <= x_hi ? (x_hi >> 2) - gl + 1 : 0;
-    rowinfo[t] = gl | (cnt << 16);
-}
-
-// A thread's stage slots of one piece: up to 4 groups of 4 source pixels.
-template <int CN>
-struct Hp3Loads {
-    uint32_t w[4][CN];
-    int32_t slot[4];   // stage slot, -1: none
-};
-
-// Groups that run past the image end (only at the window's last row, when it
-// reaches the source's right edge) are loaded dword by dword, the partial
-// dword one to three bytes early and shifted down (bytes past the end are
-// never used).
-template <int CN>
-__device__ __forceinline__ void hp3_load_tail(const Hp3Block& B, uint32_t off, uint32_t (&w)[CN]) {
-#pragma unroll
-    for (int d = 0; d < CN; ++d) {
-        const int32_t o = (int32_t)off + 4 * d;
-        uint32_t v = 0u;
-        if (o + 4 <= B.nrec) {
-            v = __builtin_amdgcn_raw_buffer_load_b32(B.rs, (uint32_t)o, 0, 0);
-        } else if (o < B.nrec) {
-            v = __builtin_amdgcn_raw_buffer_load_b32(B.rs, (uint32_t)(B.nrec - 4), 0, 0) >> (8 * (o + 4 - B.nrec));
-        }
-        w[d] = v;
-    }
-}
-
-// Issue the loads of a piece's stage slots (slot g = thread + 256 i; row
-// g / S, group g mod S).  Every rowinfo read is issued before any load.
-template <int CN>
-__device__ __forceinline__ void hp3_issue(const Hp3Block& B, const Hp3Piece& pc, const int32_t* __restrict__ rowinfo,
-                                          Hp3Loads<CN>& L) {
-    const int n = pc.rows * B.slots;
-    int32_t info[4], jv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int g = (int)threadIdx.x + HP_THREADS * i;
-        // j = g / S exactly: g < 2^12, and the fraction stays ≥ 0.5 / S from an integer
-        jv[i] = min((int)(((float)g + 0.5f) * B.rslots), HP_MAXROWS - 1);
-        info[i] = rowinfo[jv[i]];
-    }
-    bool tail = false;
-    uint32_t off[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int g = (int)threadIdx.x + HP_THREADS * i;
-        const int k = g - jv[i] * B.slots;
-        const int gl = info[i] & 0xFFFF, cnt = info[i] >> 16;
-        const bool on = g < n && k < cnt;
-        off[i] = (uint32_t)(pc.jlo + jv[i]) * (uint32_t)B.pitch + (uint32_t)(gl + k) * (uint32_t)(4 * CN);
-        L.slot[i] = on ? g : -1;
-        const bool fast = !(kHpX & 8) && on && (int32_t)off[i] + 4 * CN <= B.nrec;
-        tail |= on && !fast;
-        if (fast) {
-            if (CN == 3) {
-                typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-                const u32x3 v = __builtin_bit_cast(u32x3, __builtin_amdgcn_raw_buffer_load_b96(B.rs, off[i], 0, 0));
-                L.w[i][0] = v.x;
-                L.w[i][1] = v.y;
-                L.w[i][2] = v.z;
-            } else {
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(B.rs, off[i], 0, 0));
-#pragma unroll
-                for (int d = 0; d < CN; ++d) L.w[i][d] = v[d];
-            }
-        }
-    }
-    if (tail) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (L.slot[i] >= 0 && (int32_t)off[i] + 4 * CN > B.nrec) hp3_load_tail<CN>(B, off[i], L.w[i]);
-    }
-}
-
-// HSV of the loaded groups → stage; the row table of the piece.
-template <int NR, int MODE, int CN>
-__device__ __forceinline__ void hp3_stage(Hpass3Lds<NR>& L, const Hp3Block& B, const Hp3Piece& pc,
-                                          const int32_t* __restrict__ rowinfo, const Hp3Loads<CN>& LD) {
-    const int t = threadIdx.x;
-    if (t < pc.rows) L.rowtab[t] = 16 * (t * B.slots - (rowinfo[t] & 0xFFFF));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (LD.slot[i] < 0) continue;
-        uint32_t p[4];
-        if (CN == 3) {
-            p[0] = LD.w[i][0];
-            p[1] = __builtin_amdgcn_alignbit(LD.w[i][1], LD.w[i][0], 24);
-            p[2] = __builtin_amdgcn_alignbit(LD.w[i][2], LD.w[i][1], 16);
-            p[3] = LD.w[i][2] >> 8;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) p[k] = LD.w[i][k < CN ? k : 0];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) p[k] = stage_px<NR, MODE>(L.T, p[k]);
-        *reinterpret_cast<uint4*>(&L.stage[4 * LD.slot[i]]) = make_uint4(p[0], p[1], p[2], p[3]);
-    }
-}
-
-// Zone bits of 4 M pixels (columns x .. x + 3 of band row rw).
-template <int NR, bool ZONES>
-__device__ __forceinline__ void hp3_zones(int yrow, int x, const int32_t* zr0, const int32_t* zrh, const int32_t* zc0,
-                                          const int32_t* zcw, uint32_t (&zb)[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) zb[k] = ~0u;
-    if (!ZONES) return;
-    uint32_t zrow = 0;
-#pragma unroll
-    for (int q = 0; q < NR; ++q) zrow |= (uint32_t)((uint32_t)(yrow - zr0[q]) < (uint32_t)zrh[q]) << q;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        uint32_t zc = 0;
-#pragma unroll
-        for (int q = 0; q < NR; ++q) zc |= (uint32_t)((uint32_t)(x + k - zc0[q]) < (uint32_t)zcw[q]) << q;
-        zb[k] = zc & zrow;
-    }
-}
-
-__device__ __forceinline__ void ring_write(WinRing& win, int rw, int x, const uint32_t (&px)[4]) {
-    uint32_t ch[4];
-    transpose4(px[0], px[1], px[2], px[3], ch);
-    const int pos = x & (RING - 1);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) *reinterpret_cast<uint32_t*>(&win[c][rw][pos]) = ch[c];
-}
-
-// Gather the piece's 16 × (xb - xa) M pixels into the ring.  Unit = 4
-// consecutive columns of one row; unit u: column group u mod C/4 (a 32-lane
-// group writes one ring row's consecutive dwords, conflict-free), row
-// (u / (C/4)) mod 16, C-block u / 4C.  A live piece (≤ C columns) is ≤ 2 units
-// per thread, issued as one batch: 8 row-table reads, then 8 pixel reads.  A
-// fill run (nothing staged) may be wider.
-template <int NR, bool ZONES, int MODE>
-__device__ __forceinline__ void hp3_gather(Hpass3Lds<NR>& L, const Hp3Block& B, const Hp3Piece& pc, int nrows,
-                                           int yb, const int32_t* zr0, const int32_t* zrh, const int32_t* zc0,
-                                           const int32_t* zcw, uint32_t fill) {
-    if (kHpX & 2) return;
-    const int ncg = B.C >> 2;
-    const int fillofs = 16 * HP_SLOTS;
-    const uint8_t* stg = reinterpret_cast<const uint8_t*>(L.stage);
-    if (pc.rows == 0) {
-        // units: 16 rows × C/4 column groups per C-block
-        const int nu = 4 * B.C * ((pc.xb - pc.xa + B.C - 1) >> (B.lgcg + 2));
-        // fill run: every pixel is the fill (black); zones still decide its α
-        for (int u = threadIdx.x; u < nu; u += HP_THREADS) {
-            const int cg = u & (ncg - 1), rw = (u >> B.lgcg) & (HR - 1), cb = u >> (B.lgcg + 4);
-            const int x = pc.xa + 4 * cg + B.C * cb;
-            if (x >= pc.xb || rw >= nrows) continue;
-            uint32_t px[4];
-            if (ZONES) {
-                uint32_t zb[4];
-                hp3_zones<NR, ZONES>(yb + rw, x, zr0, zrh, zc0, zcw, zb);
-                const uint32_t v = *reinterpret_cast<const uint32_t*>(stg + fillofs);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) px[k] = window_px<NR, MODE>(L.T, v, zb[k]);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) px[k] = fill;
-            }
-            ring_write(L.win, rw, x, px);
-        }
-        return;
-    }
-    int a[2][4], xs[2], rws[2];
-    bool on[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int u = (int)threadIdx.x + HP_THREADS * i;
-        const int cg = u & (ncg - 1), rw = (u >> B.lgcg) & (HR - 1);
-        const int x = pc.xa + 4 * cg;
-        xs[i] = x;
-        rws[i] = rw;
-        on[i] = u < 4 * B.C && x < pc.xb && rw < nrows;
-        uint32_t xx = B.rowx0 + (uint32_t)rw * (uint32_t)B.b1 + (uint32_t)x * (uint32_t)B.b0;
-        uint32_t yy = B.rowy0 + (uint32_t)rw * (uint32_t)B.b4 + (uint32_t)x * (uint32_t)B.b3;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int xin = (int32_t)xx >> 16, yin = (int32_t)yy >> 16;
-            const bool ok = ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h);
-            const int jj = min(max(yin - pc.jlo, 0), pc.rows - 1);
-            // row table read now, pixel read below: all 8 in flight together
-            // (rb feeds both arms of the select, so the read is not sunk into
-            // a branch of its own)
-            const int rb = L.rowtab[jj];
-            a[i][k] = rb + (ok ? 4 * xin : fillofs - rb);
-            xx += (uint32_t)B.b0;
-            yy += (uint32_t)B.b3;
-        }
-    }
-    uint32_t v[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[i][k] = *reinterpret_cast<const uint32_t*>(stg + a[i][k]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        if (!on[i]) continue;
-        uint32_t zb[4], px[4];
-        hp3_zones<NR, ZONES>(yb + rws[i], xs[i], zr0, zrh, zc0, zcw, zb);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) px[k] = window_px<NR, MODE>(L.T, v[i][k], zb[k]);
-        ring_write(L.win, rws[i], xs[i], px);
-    }
-}
-
-// Chunks: ≤ 4 output tiles whose input window fits the ring.
-struct Hp3Chunk {
+// One chunk of ≤ 4 output tiles whose input window fits the ring.
+struct Hp2Chunk {
     int s0, s1;   // tiles [s0, s1)
-    int c0, cend; // new M columns [c0, cend)
+    int c0;       // first M column not yet in the ring
+    int ng4;      // new 4-column groups
+    int nsteps;   // this wave's phase-1 steps (16 groups per step over the block)
 };
 
-__device__ __forceinline__ Hp3Chunk hp3_chunk(const int4* hdr, int s0, int ntiles, int& filled) {
-    Hp3Chunk c;
+__device__ __forceinline__ Hp2Chunk hp2_chunk(const int4* hdr, int s0, int ntiles, int& filled, int wave) {
+    Hp2Chunk c;
     c.s0 = s0;
     const int W0 = hdr[s0].x;
     int s1 = min(s0 + 4, ntiles), W1;
@@ -537,104 +248,175 @@ __device__ __forceinline__ Hp3Chunk hp3_chunk(const int4* hdr, int s0, int ntile
     c.s1 = s1;
     if (W1 - W0 > RING && threadIdx.x == 0) atomicOr(&g_pipe_status, 1);  // single tile beyond the ring
     c.c0 = max(filled, W0);
-    c.cend = max(c.c0, W1);
+    c.ng4 = max(0, (W1 - c.c0) >> 2);
+    c.nsteps = c.ng4 > wave * 4 ? (c.ng4 - wave * 4 + 4 * HP_NW - 1) / (4 * HP_NW) : 0;
     filled = max(filled, W1);
     return c;
 }
 
-template <int NR, bool ZONES, int CN>
-__device__ __forceinline__ void hpass3_body(Hpass3Lds<NR>& L, const Hp3Block& B, uint8_t* __restrict__ tmp,
-                                            const int32_t* __restrict__ coefs, const ipp_resample_desc& h, int row0,
-                                            int nrows, const int32_t* zr0, const int32_t* zrh, const int32_t* zc0,
-                                            const int32_t* zcw, uint32_t fill) {
-    constexpr int MODE = StageMode<NR, ZONES>::v;
+template <int NR, bool ZONES, int CN, bool CLAMP>
+__device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win, int wave, const Hp2Block& B,
+                                            uint8_t* __restrict__ tmp,
+                                            const int32_t* __restrict__ coefs, const ipp_resample_desc& h,
+                                            int row0, int nrows, const int32_t* zc0, const int32_t* zcw,
+                                            uint32_t zrow, uint32_t fill) {
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = 2 * (lane >> 3) + ((lane >> 1) & 1);  // the lane's window row
     const int ntiles = (h.out_len + 15) >> 4;
     const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
     const int32_t* tbias = coefs + h.coef_off + 4 * (int64_t)ntiles;
     const uint4* tblk = reinterpret_cast<const uint4*>(coefs + h.coef_off + 20 * (int64_t)ntiles);
-    const int yb = h.line0 + row0;  // M row of the band's row 0
-    const int C = B.C;
+    const uint32_t sx = (uint32_t)HP_STEPC * (uint32_t)B.b0, sy = (uint32_t)HP_STEPC * (uint32_t)B.b3;  // per-step advance
 
-    // Piece generator over the chunks.  A piece is ≤ C live columns, or a
-    // fill run (columns outside the band's valid range [xlo, xhi], nothing to
-    // stage) up to the next live column or the chunk's end; a chunk with no
-    // new columns still yields one empty piece, so its phase 2 runs.
-    int filled = hdr[0].x;
-    Hp3Chunk gch = hp3_chunk(hdr, 0, ntiles, filled);
-    int gx = gch.c0;
-    bool gemitted = false;
-    auto gen = [&](Hp3Piece& p) -> bool {
-        if (gx >= gch.cend && gemitted) {
-            if (gch.s1 >= ntiles) return false;
-            gch = hp3_chunk(hdr, gch.s1, ntiles, filled);
-            gx = gch.c0;
-            gemitted = false;
+    int filled = hdr[0].x;  // ring holds M columns [.., filled)
+    Hp2Chunk ck = hp2_chunk(hdr, 0, ntiles, filled, wave);
+    // Lane's first column of step 0 and its source position.
+    auto lane_x = [&](const Hp2Chunk& c) { return c.c0 + 16 * wave + 8 * ((lane >> 2) & 1) + (lane & 1); };
+    // (24-bit products: columns < 2^15 and |b| ≤ 2^16; a 32-bit product made
+    // the compiler use a 64-bit mad whose unused high addend was a register
+    // that can still be in flight)
+    int xl = lane_x(ck);
+    uint32_t xxl = B.rowx + (uint32_t)__mul24(xl, B.b0), yyl = B.rowy + (uint32_t)__mul24(xl, B.b3);
+    Raw4 RA, RB, RC;
+    RA.live = RB.live = RC.live = false;
+    RA.fl = RB.fl = RC.fl = 0u;
+    // A step = 16 columns of 16 rows per wave; steps past the chunk or wholly
+    // outside the band's valid columns are dead: no gathers, no HSV, constant
+    // window bytes.
+    auto issue = [&](const Hp2Chunk& c, int st, uint32_t xx, uint32_t yy, Raw4& o) {
+        const int xs = c.c0 + 16 * wave + HP_STEPC * st;
+        const bool live = st < c.nsteps && xs + 15 >= B.xlo && xs <= B.xhi;
+        if (!live) {
+            o.any = false;
+            o.live = false;
+            return;
         }
-        p.xa = gx;
-        int xb;
-        if (gx > B.xhi) xb = gch.cend;                                          // past the live columns
-        else if (gx + C <= B.xlo) xb = min(gch.cend, max(gx + 4, B.xlo & ~3));  // before them
-        else xb = min(gx + C, gch.cend);
-        p.xb = max(gx, xb);
-        gx = p.xb;
-        gemitted = true;
-        p.s0 = gch.s0;
-        p.s1 = gch.s1;
-        p.last = gx >= gch.cend;
-        return true;
+        hp2_issue<CN, CLAMP>(B, xx, yy, o);
     };
-    auto spans = [&](Hp3Piece& p, int par) {
-        hp3_spans(B, max(p.xa, B.xlo), min(p.xb, B.xhi + 1), L.rowinfo[par], p);
-    };
+    issue(ck, 0, xxl, yyl, RA);
+    issue(ck, 1, xxl + sx, yyl + sy, RB);
 
-    Hp3Piece q, nq, nnq;
-    gen(q);
-    spans(q, 0);
-    bool hnq = gen(nq);
-    if (hnq) spans(nq, 1);
-    __syncthreads();
-    Hp3Loads<CN> LD;
-    hp3_issue<CN>(B, q, L.rowinfo[0], LD);
-    hp3_stage<NR, MODE, CN>(L, B, q, L.rowinfo[0], LD);
-    if (hnq) hp3_issue<CN>(B, nq, L.rowinfo[1], LD);
-    __syncthreads();
-    int par = 0;  // q's rowinfo buffer
     for (;;) {
-        // ---- A: spans of q+2; q → ring; taps of q's chunk
-        const bool hnnq = hnq && gen(nnq);
-        if (hnnq) spans(nnq, par);
-        const int t = q.s0 + wave;
-        const bool has_tile = !(kHpX & 4) && q.last && t < q.s1;
+        // This wave's tile taps for the first K step, in flight during phase 1.
+        const int t = ck.s0 + wave;
+        const bool has_tile = t < ck.s1 && nrows > 0;
         int4 th = make_int4(0, 0, 0, 0);
         uint4 bn[3];
-        int32_t bias = 0;
+        int32_t bias = 0;  // the lane's output column bias, in flight with the taps
         const uint4* bt = tblk + lane;
-        if (has_tile) {
-            th = hdr[t];
+        {
+            // Loaded unconditionally (a valid tile stands in when the wave
+            // has none), so the loads in flight do not depend on the path.
+            const int te = min(t, ntiles - 1);
+            th = hdr[te];
             bt += th.z;
 #pragma unroll
             for (int p = 0; p < 3; ++p) bn[p] = bt[p * 64];
-            bias = tbias[min(16 * t + (lane & 15), h.out_len - 1)];
+            const int xb = 16 * te + (lane & 15);
+            bias = tbias[min(xb, h.out_len - 1)];
+            if (!has_tile) th.y = 0;
         }
-        hp3_gather<NR, ZONES, MODE>(L, B, q, nrows, yb, zr0, zrh, zc0, zcw, fill);
+
+        // Phase 1: new M columns → planar LDS ring.  Three register sets
+        // rotate so that each step's gathers have two steps of HSV work to land.
+        const int c0 = ck.c0, ng4 = ck.ng4, nsteps = ck.nsteps;
+        // newer = gather loads issued after P's (4 per live later set)
+        auto process = [&](Raw4& P, int st, int newer) {
+            asm_wait(P.p, P.live ? newer : -1);
+            // after the pair exchange lane dx holds columns 8gc + 4dx .. +3
+            const int cg = wave * 4 + 4 * HP_NW * st + 2 * ((lane >> 2) & 1) + (lane & 1);
+            const int x = c0 + 4 * cg;
+            const bool active = (cg < ng4) && (r < nrows);
+            uint32_t px[4], zb[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                zb[k] = ~0u;
+                if (ZONES) {
+                    // column of gather k's pixel (before the pair exchange)
+                    const int xk = c0 + 16 * wave + HP_STEPC * st + 8 * ((lane >> 2) & 1) + (lane & 1) + 2 * k;
+                    zb[k] = 0;
+#pragma unroll
+                    for (int q = 0; q < NR; ++q) zb[k] |= (uint32_t)((uint32_t)(xk - zc0[q]) < (uint32_t)zcw[q]) << q;
+                    zb[k] &= zrow;
+                }
+            }
+            // One branch per step (not per pixel) so the four pixels' table
+            // reads and arithmetic interleave in one basic block.
+            uint32_t ch[4];
+            if (__builtin_amdgcn_ballot_w64(P.any) != 0ull) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    uint32_t raw = P.p[k];
+                    if (CLAMP) raw >>= ((P.fl >> (1 + k)) & 1u) << 3;
+                    px[k] = hsv2_px<NR, ZONES>(T, raw, zb[k]);
+                }
+                pair_regroup(px, lane & 1);
+                transpose4(px[0], px[1], px[2], px[3], ch);
+            } else if (ZONES) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) px[k] = hsv2_px<NR, ZONES>(T, 0u, zb[k]);
+                pair_regroup(px, lane & 1);
+                transpose4(px[0], px[1], px[2], px[3], ch);
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) ch[c] = ((fill >> (8 * c)) & 0xFFu) * 0x01010101u;
+            }
+            if (active) {
+                const int pos = x & (RING - 1);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) *reinterpret_cast<uint32_t*>(&win[c][r][pos]) = ch[c];
+            }
+        };
+        auto iss = [&](int st2, Raw4& o) { issue(ck, st2, xxl + st2 * sx, yyl + st2 * sy, o); };
+        // The loop runs whole register-set rotations (a trailing step past
+        // nsteps is dead).  With no early exit each set keeps its registers;
+        // an exit mid-rotation made the compiler shuffle the sets through
+        // copies, and copying a register whose load is in flight waits for it.
+        for (int st = 0; st < nsteps; st += 3) {
+            iss(st + 2, RC);
+            process(RA, st, 4 * (RB.live + RC.live));
+            iss(st + 3, RA);
+            process(RB, st + 1, 4 * (RC.live + RA.live));
+            iss(st + 4, RB);
+            process(RC, st + 2, 4 * (RA.live + RB.live));
+        }
+
+        // The chunk's first tap and bias loads (issued before its gathers) are
+        // waited for here on every path: a compiler wait for them after the
+        // next chunk's asm gathers would drain those as well.
+        asm volatile("" ::"v"(bn[0].x), "v"(bn[1].x), "v"(bn[2].x), "v"(bias));
+        // Next chunk's first steps, issued now so they fly during phase 2
+        // (whose K-step tap loads, issued after them, then wait for them too:
+        // vmcnt retires in order).  (Issuing them after the MFMAs, with the
+        // accumulators live, let the compiler move the in-flight gather
+        // registers and broke parity.)
+        const int s1 = ck.s1;
+        const bool more = s1 < ntiles;
+        if (more) {
+            ck = hp2_chunk(hdr, s1, ntiles, filled, wave);
+            xl = lane_x(ck);
+            xxl = B.rowx + (uint32_t)__mul24(xl, B.b0);
+            yyl = B.rowy + (uint32_t)__mul24(xl, B.b3);
+        } else {
+            ck.nsteps = 0;  // no loads
+        }
+        issue(ck, 0, xxl, yyl, RA);
+        issue(ck, 1, xxl + sx, yyl + sy, RB);
         __syncthreads();
-        // ---- B: q+1 → stage; loads of q+2 (in flight until the next B);
-        // phase 2 at a chunk's end
-        if (hnq) hp3_stage<NR, MODE, CN>(L, B, nq, L.rowinfo[par ^ 1], LD);
-        if (hnnq) hp3_issue<CN>(B, nnq, L.rowinfo[par], LD);
+
+        // Phase 2 (mfma): wave w takes tile s0 + w; A = 16 window rows × 64
+        // columns of one channel (lane l: row l&15, bytes 16(l>>4)..+15),
+        // B = 64 columns × 16 outputs of one tap byte plane.  D lane l =
+        // output l&15, rows 4(l>>4)..+3 = exactly one 16-B T group.  The
+        // column bias rides in the first byte plane's initial accumulator.
         if (has_tile) {
-            // Phase 2 (mfma): wave w takes tile s0 + w; A = 16 window rows ×
-            // 64 columns of one channel (lane l: row l&15, bytes
-            // 16(l>>4)..+15), B = 64 columns × 16 outputs of one tap byte
-            // plane.  D lane l = output l&15, rows 4(l>>4)..+3 = exactly one
-            // 16-B T group.
             i32x4 acc[4][3];
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-#pragma unroll
-                for (int p = 0; p < 3; ++p) acc[c][p] = i32x4{0, 0, 0, 0};
+            for (int c = 0; c < 4; ++c) {
+                acc[c][0] = i32x4{bias, bias, bias, bias};
+                acc[c][1] = i32x4{0, 0, 0, 0};
+                acc[c][2] = i32x4{0, 0, 0, 0};
+            }
             const int arow = lane & 15, akoff = 16 * (lane >> 4);
 #pragma unroll 1
             for (int ks = 0; ks < th.y; ++ks) {
@@ -648,7 +430,7 @@ __device__ __forceinline__ void hpass3_body(Hpass3Lds<NR>& L, const Hp3Block& B,
                 const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const i32x4 a = *reinterpret_cast<const i32x4*>(&L.win[c][arow][pos]);
+                    const i32x4 a = *reinterpret_cast<const i32x4*>(&win[c][arow][pos]);
 #pragma unroll
                     for (int p = 0; p < 3; ++p)
                         acc[c][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[p], acc[c][p], 0, 0, 0);
@@ -661,7 +443,7 @@ __device__ __forceinline__ void hpass3_body(Hpass3Lds<NR>& L, const Hp3Block& B,
                 for (int c = 0; c < 4; ++c)
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr) {
-                        const int32_t ss = bias + acc[c][0][rr] + (acc[c][1][rr] << 8) + (acc[c][2][rr] << 16);
+                        const int32_t ss = acc[c][0][rr] + (acc[c][1][rr] << 8) + (acc[c][2][rr] << 16);
                         outc[c] |= clip8(ss) << (8 * rr);
                     }
                 const int grp = (row0 >> 2) + (lane >> 4);
@@ -670,19 +452,21 @@ __device__ __forceinline__ void hpass3_body(Hpass3Lds<NR>& L, const Hp3Block& B,
                                   outc[3] ^ 0x80808080u);
             }
         }
+        // The next chunk's first sets are waited for here, at the end of
+        // phase 2 (which hid their latency): from this point on the compiler
+        // may copy their registers (it does, at the loop's back edge).
+        asm_wait(RA.p, RA.live ? 4 * RB.live : -1);
+        asm_wait(RB.p, RB.live ? 0 : -1);
+        if (!more) break;
         __syncthreads();
-        if (!hnq) break;
-        q = nq;
-        nq = nnq;
-        hnq = hnnq;
-        par ^= 1;
     }
 }
 
 // Composite rows outside the overlay's 16-row bands [vb0, vb1) are plain
-// copies of the background (Paste.c leaves them untouched).  Dedicated copy
-// blocks of the H-pass launch write them, so ipp_pipe_vblend_bands then only
-// visits the bands the overlay touches.
+// copies of the background (Paste.c leaves them untouched).  The H-pass
+// blocks of an item share that copy (block `share` of `nshare`): it rides on a
+// memory system the VALU-bound H pass leaves idle, and ipp_pipe_vblend_bands
+// then only visits the bands the overlay touches.
 __device__ __forceinline__ void paste_bands(const ipp_paste_desc& p, int& vb0, int& vb1) {
     vb0 = (p.y >> 4) << 4;
     vb1 = min(p.bg_h, ((p.y + p.ov_h + 15) >> 4) << 4);
@@ -740,12 +524,14 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
     }
 }
 
+// 4 waves per SIMD (≤ 128 VGPRs); the > 8-range zone forms get 3 (they spill
+// at 128, and nothing may spill between an asm gather and its wait).
 template <int NR, bool ZONES, int CN, bool COPY>
-__global__ void __launch_bounds__(HP_THREADS) __attribute__((amdgpu_waves_per_eu(3)))
-k_pipe_hpass3(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
+__global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES && NR > 8 ? 3 : 4)))
+k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
               const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp, const uint8_t* __restrict__ bg,
               uint8_t* __restrict__ dst, int cpi) {
-    __shared__ Hpass3Lds<NR> L;
+    __shared__ Hpass2Lds<NR> L;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     // tiles_y = H-pass blocks per item.  COPY: each item owns tiles_y H-pass
     // blocks followed by cpi background-copy blocks, so the copies run beside
@@ -754,64 +540,66 @@ k_pipe_hpass3(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
     const int im = b / per_item;
     const int tb = b - im * per_item;
     if (COPY && tb >= tiles_y) {
-        bg_copy_outside_bands<HP_THREADS>(descs[im].p, bg, dst, tb - tiles_y, cpi);
+        bg_copy_outside_bands<64 * HP_NW>(descs[im].p, bg, dst, tb - tiles_y, cpi);
         return;
     }
     const ipp_gather_desc g = descs[im].g;
     const ipp_resample_desc h = descs[im].h;
     const int row0 = tb * HR;
     if (row0 >= h.lines) return;  // block-uniform
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
     hsv_tables_init<NR>(L.T, hp);
 
-    // Zones (filtres_liste.py:102-103): per range the M rows [zr0, zr0 + zrh)
-    // and columns [zc0, zc0 + zcw).
-    int32_t zr0[ZONES ? NR : 1], zrh[ZONES ? NR : 1], zc0[ZONES ? NR : 1], zcw[ZONES ? NR : 1];
+    // Zones: per-lane row bits now, column bits per pixel.  With > 8 ranges
+    // the column bounds live in LDS (in registers they spilled).
+    int32_t zc0r[ZONES && NR <= 8 ? NR : 1], zcwr[ZONES && NR <= 8 ? NR : 1];
+    int32_t* zc0 = zc0r;
+    int32_t* zcw = zcwr;
+    if (ZONES && NR > 8) {
+        zc0 = L.zc;
+        zcw = L.zc + NR;
+    }
+    uint32_t zrow = 0;
+    const int lane = threadIdx.x & 63;
+    const int y = h.line0 + row0 + 2 * (lane >> 3) + ((lane >> 1) & 1);
     if (ZONES) {
 #pragma unroll
         for (int k = 0; k < NR; ++k) {
             int a, bb, cc, dd;
             slice_indices(hp.r[k].zone[0], g.out_h - hp.r[k].zone[1], g.out_h, a, bb);
             slice_indices(hp.r[k].zone[2], g.out_w - hp.r[k].zone[3], g.out_w, cc, dd);
-            zr0[k] = a;
-            zrh[k] = bb - a;
-            zc0[k] = cc;
-            zcw[k] = dd - cc;
+            zrow |= (uint32_t)(y >= a && y < bb) << k;
+            if (NR <= 8 || threadIdx.x == 0) {
+                zc0[k] = cc;
+                zcw[k] = dd - cc;
+            }
         }
     }
 
-    // Source window as a buffer resource (32-bit scalar arithmetic: a 64-bit
-    // value would land in VGPRs and turn every buffer load into a waterfall
-    // loop; items are < 2 GiB, checked on the host).
+    // Source window as a buffer resource: every in-window dword read is in
+    // range; out-of-window pixels use offset 0xFFFFFFFF (range check → 0).
     const Sampler S = make_sampler(src, g);
+    // (32-bit scalar arithmetic: a 64-bit min would land in VGPRs and turn every
+    // buffer load into a waterfall loop; items are < 2 GiB, checked on the host.)
     const int nrec = (g.src_h - g.in_y0) * g.src_pitch - g.in_x0 * g.src_cn;
+    const int need = (g.in_h - 1) * g.src_pitch + g.in_w * CN + (CN == 3 ? 1 : 0);
+    const bool clamp = need > nrec;  // last pixel's dword would cross the image end (block-uniform)
     const uint64_t sbu = reinterpret_cast<uint64_t>(S.base);
-    Hp3Block B;
-    B.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(sbu), (short)0, nrec, 0x00020000);
-    B.nrec = nrec;
-    const int y0 = h.line0 + row0;
-    B.rowx0 = (uint32_t)S.b2 + (uint32_t)y0 * (uint32_t)S.b1;
-    B.rowy0 = (uint32_t)S.b5 + (uint32_t)y0 * (uint32_t)S.b4;
+    Hp2Block B;
+    B.rsv = u32x4_t{(uint32_t)sbu, (uint32_t)(sbu >> 32) & 0xFFFFu, (uint32_t)nrec, 0x00020000u};
+    B.lim = S.lim;
+    B.rowx = (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1;
+    B.rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
     B.b0 = S.b0;
-    B.b1 = S.b1;
     B.b3 = S.b3;
-    B.b4 = S.b4;
     B.pitch = (int32_t)S.pitch;
     B.in_w = S.in_w;
     B.in_h = S.in_h;
-    hp3_layout(B);
-    B.bad = B.C == 0 || S.in_w > 32767;  // not a rotation, or columns beyond the 16-bit span fields
-    if (B.bad) {
-        if (threadIdx.x == 0) atomicOr(&g_pipe_status, 2);
-        B.C = HP_CMAX;
-        B.lgcg = 5;
-    }
     {
-        // Row r's valid columns: 0 <= xx(x) < in_w·2^16 and 0 <= yy(x) < in_h·2^16,
-        // both linear in x; ±2 columns of slack absorb the rounding.  Union
-        // over the band's 16 rows (lane r holds row r) by readlane.
-        const int r = threadIdx.x & 15;
-        const uint32_t rx = B.rowx0 + (uint32_t)r * (uint32_t)B.b1, ry = B.rowy0 + (uint32_t)r * (uint32_t)B.b4;
+        // Row y's valid columns: 0 <= xx(x) < in_w·2^16 and 0 <= yy(x) < in_h·2^16,
+        // both linear in x; ±2 columns of slack absorb the rounding.  Union over
+        // the block's 16 rows (lanes 8(r>>1) + 2(r&1) .. hold row r) by readlane.
         float lo = -1e9f, hi = 1e9f;
         auto clip = [&](float a, float bb, float lim) {
             if (bb == 0.0f) {
@@ -822,28 +610,29 @@ k_pipe_hpass3(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
                 hi = fminf(hi, fmaxf(t1, t2));
             }
         };
-        clip((float)(int32_t)rx, (float)S.b0, 65536.0f * (float)S.in_w);
-        clip((float)(int32_t)ry, (float)S.b3, 65536.0f * (float)S.in_h);
+        clip((float)(int32_t)B.rowx, (float)S.b0, 65536.0f * (float)S.in_w);
+        clip((float)(int32_t)B.rowy, (float)S.b3, 65536.0f * (float)S.in_h);
         const int ilo = lo > hi ? 0x3FFFFFFF : (int)fmaxf(lo - 2.0f, -1e8f);
         const int ihi = lo > hi ? -0x3FFFFFFF : (int)fminf(hi + 2.0f, 1e8f);
         int blo = 0x3FFFFFFF, bhi = -0x3FFFFFFF;
 #pragma unroll
         for (int rr = 0; rr < HR; ++rr) {
-            blo = min(blo, __builtin_amdgcn_readlane(ilo, rr));
-            bhi = max(bhi, __builtin_amdgcn_readlane(ihi, rr));
+            const int lr = 8 * (rr >> 1) + 2 * (rr & 1);  // a lane of row rr
+            blo = min(blo, __builtin_amdgcn_readlane(ilo, lr));
+            bhi = max(bhi, __builtin_amdgcn_readlane(ihi, lr));
         }
         B.xlo = blo;
         B.xhi = bhi;
     }
 
     __syncthreads();  // tables visible
-    // Fill (raw 0 = black, rotations.py's transparent fill read back without
-    // alpha): uniform over the block except for zone bits.
-    constexpr int MODE = StageMode<NR, ZONES>::v;
-    const uint32_t fill = hsv2_px<NR, false>(L.T, 0u, ~0u);
-    if (threadIdx.x == 0) L.stage[4 * HP_SLOTS] = stage_px<NR, MODE>(L.T, 0u);
+    // Fill value (raw 0): uniform over the block except for zone bits.
+    const uint32_t fill = hsv2_px<NR, ZONES>(L.T, 0u, ~0u);
     const int nrows = min(HR, h.lines - row0);
-    hpass3_body<NR, ZONES, CN>(L, B, tmp, coefs, h, row0, nrows, zr0, zrh, zc0, zcw, fill);
+    if (CN == 3 && clamp)
+        hpass2_body<NR, ZONES, CN, true>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+    else
+        hpass2_body<NR, ZONES, CN, false>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
 }
 
 // V pass on MFMA (tap tiles aligned with 16-row background bands: the plan's
@@ -979,11 +768,11 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
     const int n = grid.x / ty;
     if (bg && dst) {  // H pass + the background rows outside the overlay bands
         const int cpi = copy_blocks_per_item();
-        hipLaunchKernelGGL((k_pipe_hpass3<NR, ZONES, CN, true>), dim3((uint32_t)(n * (ty + cpi))), dim3(HP_THREADS), 0,
+        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, true>), dim3((uint32_t)(n * (ty + cpi))), dim3(64 * HP_NW), 0,
                            s, src, tmp, coefs, descs, ty, hp, bg, dst, cpi);
         return;
     }
-    hipLaunchKernelGGL((k_pipe_hpass3<NR, ZONES, CN, false>), grid, dim3(HP_THREADS), 0, s, src, tmp, coefs, descs, ty,
+    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, false>), grid, dim3(64 * HP_NW), 0, s, src, tmp, coefs, descs, ty,
                        hp, bg, dst, 0);
 }
 
