@@ -62,6 +62,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-sample", type=int, default=192)
     ap.add_argument("--no-copy-ceiling", action="store_true")
     ap.add_argument("--unsplit", action="store_true", help="pipe5: ipp_pipe_hpass + full-frame ipp_pipe_vblend")
+    ap.add_argument("--split", action="store_true",
+                    help="pipe5: ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands (two launches) instead of ipp_pipe_fused")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: CPU rehearsal of the N-rank path (tests)")
     ap.add_argument("--dump-digests", default=None,
@@ -284,7 +286,11 @@ def main(argv=None):
                        for i, p in enumerate(plan.params)}
         else:
             runner = fused.PipeRunner(plan, dev)
-            if runner.split and not args.unsplit:
+            if runner.split and not args.unsplit and not args.split:
+                # one launch: H pass, background copy, V pass + paste (ipp_pipe_fused)
+                algo = {"ipp_pipe_fused": plan.algo_bytes_hpass_bgcopy + plan.algo_bytes_vblend_bands}
+                launches = [("ipp_pipe_fused", lambda: runner.fused(src, bgs, out))]
+            elif runner.split and not args.unsplit:
                 # the H pass also copies the background rows outside the overlay bands
                 algo = {"ipp_pipe_hpass_bgcopy": plan.algo_bytes_hpass_bgcopy,
                         "ipp_pipe_vblend_bands": plan.algo_bytes_vblend_bands}

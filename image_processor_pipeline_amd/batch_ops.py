@@ -103,12 +103,12 @@ def keep_largest(imgs: Sequence[np.ndarray]) -> List[Optional[np.ndarray]]:
     """pixels_isolés.py:29-81 for a chunk of BGRA images: one
     ipp_ccl_keep_largest launch, then one crop launch; None where no pixel
     is left (the reference's boundingRect(None) raises there)."""
-    from .device_ccl import keep_largest_masks
+    from .device_ccl import keep_largest_packed
     if not imgs:
         return []
     src, soffs = _pack(imgs)
-    views = [src[o:o + im.nbytes].view(im.shape) for o, im in zip(soffs, imgs)]
-    bbs = keep_largest_masks(views)
+    # in place on the packed chunk (no second device copy of the images)
+    bbs = keep_largest_packed(src, soffs, [(im.shape[0], im.shape[1]) for im in imgs])
     jobs = [(i, (b[0], b[1], b[2] - b[0], b[3] - b[1]), 0) for i, b in enumerate(bbs) if b is not None]
     if not jobs:
         return [None] * len(imgs)

@@ -254,7 +254,7 @@ __device__ __forceinline__ Hp2Chunk hp2_chunk(const int4* hdr, int s0, int ntile
     return c;
 }
 
-template <int NR, bool ZONES, int CN, bool CLAMP>
+template <int NR, bool ZONES, int CN, bool CLAMP, bool SC1>
 __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win, int wave, const Hp2Block& B,
                                             uint8_t* __restrict__ tmp,
                                             const int32_t* __restrict__ coefs, const ipp_resample_desc& h,
@@ -448,8 +448,11 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                     }
                 const int grp = (row0 >> 2) + (lane >> 4);
                 uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
-                *dst = make_uint4(outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
-                                  outc[3] ^ 0x80808080u);
+                const uint32_t w[4] = {outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
+                                       outc[3] ^ 0x80808080u};
+                // SC1 (fused launch): written through to memory, for the V
+                // blocks of another CU / XCD that read it in the same launch
+                store16<SC1 ? 1 : 0>(reinterpret_cast<uint8_t*>(dst), 16, true, w);
             }
         }
         // The next chunk's first sets are waited for here, at the end of
@@ -524,25 +527,15 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
     }
 }
 
-// 4 waves per SIMD (≤ 128 VGPRs); the > 8-range zone forms get 3 (they spill
-// at 128, and nothing may spill between an asm gather and its wait).
-template <int NR, bool ZONES, int CN, bool COPY>
-__global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES && NR > 8 ? 3 : 4)))
-k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
-              const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp, const uint8_t* __restrict__ bg,
-              uint8_t* __restrict__ dst, int cpi) {
-    __shared__ Hpass2Lds<NR> L;
-    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    // tiles_y = H-pass blocks per item.  COPY: each item owns tiles_y H-pass
-    // blocks followed by cpi background-copy blocks, so the copies run beside
-    // the H pass on every XCD.
-    const int per_item = tiles_y + (COPY ? cpi : 0);
-    const int im = b / per_item;
-    const int tb = b - im * per_item;
-    if (COPY && tb >= tiles_y) {
-        bg_copy_outside_bands<64 * HP_NW>(descs[im].p, bg, dst, tb - tiles_y, cpi);
-        return;
-    }
+// One H-pass block: band tb of item im.  SYNC (fused launch): T is stored
+// write-through and, once every wave's stores have drained, the block adds one
+// to the item's completion counter (agent scope) — the hand-off protocol of
+// MI355X_MICROARCH.md §Correctness boundaries for a consumer on any CU / XCD.
+template <int NR, bool ZONES, int CN, bool SYNC>
+__device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __restrict__ src,
+                                            uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
+                                            const ipp_pipe_desc* __restrict__ descs, int im, int tb,
+                                            const ipp_hsv_params& hp, int32_t* __restrict__ done) {
     const ipp_gather_desc g = descs[im].g;
     const ipp_resample_desc h = descs[im].h;
     const int row0 = tb * HR;
@@ -630,9 +623,36 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
     const uint32_t fill = hsv2_px<NR, ZONES>(L.T, 0u, ~0u);
     const int nrows = min(HR, h.lines - row0);
     if (CN == 3 && clamp)
-        hpass2_body<NR, ZONES, CN, true>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+        hpass2_body<NR, ZONES, CN, true, SYNC>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
     else
-        hpass2_body<NR, ZONES, CN, false>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+        hpass2_body<NR, ZONES, CN, false, SYNC>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+    if (SYNC) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's T stores have reached memory
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(done + im, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// 4 waves per SIMD (≤ 128 VGPRs); the > 8-range zone forms get 3 (they spill
+// at 128, and nothing may spill between an asm gather and its wait).
+template <int NR, bool ZONES, int CN, bool COPY>
+__global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES && NR > 8 ? 3 : 4)))
+k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
+              const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp, const uint8_t* __restrict__ bg,
+              uint8_t* __restrict__ dst, int cpi) {
+    __shared__ Hpass2Lds<NR> L;
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    // tiles_y = H-pass blocks per item.  COPY: each item owns tiles_y H-pass
+    // blocks followed by cpi background-copy blocks, so the copies run beside
+    // the H pass on every XCD.
+    const int per_item = tiles_y + (COPY ? cpi : 0);
+    const int im = b / per_item;
+    const int tb = b - im * per_item;
+    if (COPY && tb >= tiles_y) {
+        bg_copy_outside_bands<64 * HP_NW>(descs[im].p, bg, dst, tb - tiles_y, cpi);
+        return;
+    }
+    hpass_block<NR, ZONES, CN, false>(L, src, tmp, coefs, descs, im, tb, hp, nullptr);
 }
 
 // V pass on MFMA (tap tiles aligned with 16-row background bands: the plan's
@@ -642,16 +662,63 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
 // step), B = 64 T rows × 16 overlay columns of one channel (four 16-B T groups
 // per lane give all four channels), D lane l = column l&15, rows 4(l>>4)..+3.
 constexpr int VBR = 16;
+// Diagnostic builds only (-DIPP_DIAG -DIPP_VB_X=…, wrong output): bit 0 = no
+// blend, bit 1 = no unpremultiply, bit 2 = no background copy loop.
+#if defined(IPP_DIAG) && defined(IPP_VB_X)
+constexpr int kVbX = IPP_VB_X;
+#else
+constexpr int kVbX = 0;
+#endif
 
-template <int STORE, int DBG = 0, bool BANDS = false>
-__global__ void __launch_bounds__(256)
-k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
-                   const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int tiles_y,
-                   int ov_w_max) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t orow[];  // [VBR][ov_w_max]
-    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / tiles_y;
-    const int ty = b - im * tiles_y;
+// orow (the band's unpremultiplied overlay rows in LDS) is indexed by
+// composite column - (p.x & ~15), so a 16-pixel composite group reads its 16
+// overlay pixels with four aligned ds_read_b128; the ≤ 15 columns before the
+// overlay and after it are zero (α 0: the background stays).
+__host__ __device__ constexpr int orow_stride(int ov_w_max) { return (ov_w_max + 32 + 3) & ~3; }
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// Paste.c BLEND on two bytes at once (16-bit lanes): DIV255(bg·(255 - a) +
+// ov·a), written as 255·bg + 128 + (ov - bg)·a (mod 2^16: the true value is
+// in [0, 65153]) followed by DIV255's (t + (t >> 8)) >> 8.
+__device__ __forceinline__ uint32_t blend_u16x2(uint32_t bg, uint32_t ov, uint32_t al) {
+    const u16x2 b = __builtin_bit_cast(u16x2, bg), o = __builtin_bit_cast(u16x2, ov), a = __builtin_bit_cast(u16x2, al);
+    const u16x2 c255 = {255, 255}, c128 = {128, 128}, c8 = {8, 8};
+    const u16x2 t = (u16x2)(o - b) * a + (b * c255 + c128);
+    return __builtin_bit_cast(uint32_t, (u16x2)((u16x2)(t + (t >> c8)) >> c8));
+}
+
+// 16 composite pixels (48 bytes, bg[0..11]) blended in place with 16 RGBA
+// overlay pixels (ov[0..15]).  Byte j of the row segment is channel j mod 3
+// of pixel j / 3; each output dword is done as two byte pairs (bytes 0, 2 and
+// 1, 3) in 16-bit lanes, the overlay byte and its pixel's α gathered by v_perm.
+__device__ __forceinline__ void blend48(uint32_t (&bg)[12], const uint32_t (&ov)[16]) {
+#pragma unroll
+    for (int d = 0; d < 12; ++d) {
+        uint32_t r[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int j0 = 4 * d + h, j1 = j0 + 2;                 // the pair's bytes
+            const int p0 = j0 / 3, p1 = j1 / 3, c0 = j0 % 3, c1 = j1 % 3;
+            // v_perm(hi, lo, sel): bytes 0-3 of lo = sel 0-3, of hi = 4-7; 0x0c = 0
+            const uint32_t sel_ov = (uint32_t)c0 | 0x0c00u | ((uint32_t)(p1 == p0 ? c1 : 4 + c1) << 16) | 0x0c000000u;
+            const uint32_t sel_al = 3u | 0x0c00u | ((uint32_t)(p1 == p0 ? 3 : 7) << 16) | 0x0c000000u;
+            const uint32_t ovp = __builtin_amdgcn_perm(ov[p1], ov[p0], sel_ov);
+            const uint32_t alp = __builtin_amdgcn_perm(ov[p1], ov[p0], sel_al);
+            const uint32_t bgp = __builtin_amdgcn_perm(0u, bg[d], h ? 0x0c030c01u : 0x0c020c00u);
+            r[h] = blend_u16x2(bgp, ovp, alp);
+        }
+        bg[d] = __builtin_amdgcn_perm(r[1], r[0], 0x06020400u);  // r0 b0, r1 b0, r0 b2, r1 b2
+    }
+}
+
+// One V-pass block: 16-row band ty of item im (BANDS: counted from the first
+// overlay band).  SC1: T is read past the caches (the fused launch's hand-off).
+template <int STORE, int DBG, bool BANDS, bool SC1>
+__device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const uint8_t* __restrict__ tmp,
+                                             const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
+                                             const int32_t* __restrict__ coefs,
+                                             const ipp_pipe_desc* __restrict__ descs, int im, int ty, int ov_w_max) {
     const ipp_paste_desc p = descs[im].p;
     int y0 = ty * VBR;
     if (BANDS) {  // only the 16-row bands the overlay touches (the rest: ipp_pipe_hpass_bgcopy)
@@ -667,7 +734,14 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
+    const int os = orow_stride(ov_w_max), xo = p.x & 15;  // orow column of overlay column 0
     if (any) {
+        // zero the ≤ 15 columns before the overlay and the 16 after it
+        for (int e = threadIdx.x; e < VBR * 32; e += 256) {
+            const int row = e >> 5, c = e & 31;
+            if (c < xo) orow[row * os + c] = 0u;
+            else if (c >= 16) orow[row * os + xo + p.ov_w + c - 16] = 0u;
+        }
         const ipp_resample_desc v = descs[im].v;
         const int phase = p.y & 15;
         const int ntiles = (v.out_len + phase + 15) >> 4;
@@ -679,26 +753,45 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
         const int ctiles = (p.ov_w + 15) >> 4;
         const int gstride = v.src_pitch >> 4;  // uint4 per T group row
         const int x_l = lane & 15;
+        // the row biases ride in the first byte plane's initial accumulators
+        int32_t rb[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rb[r] = tbias[16 * t + 4 * (lane >> 4) + r];
+        const uint64_t tbase = reinterpret_cast<uint64_t>(tmp + v.src_off);
+        const __amdgpu_buffer_rsrc_t trs =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(tbase), (short)0, 0x7FFFFFFF, 0x00020000);
         for (int ct = wave; ct < ctiles; ct += 4) {
             const int x = 16 * ct + x_l;
             const int xs = min(x, p.ov_w - 1);
             i32x4 acc[4][3];
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-#pragma unroll
-                for (int q = 0; q < 3; ++q) acc[c][q] = i32x4{0, 0, 0, 0};
+            for (int c = 0; c < 4; ++c) {
+                acc[c][0] = i32x4{rb[0], rb[1], rb[2], rb[3]};
+                acc[c][1] = i32x4{0, 0, 0, 0};
+                acc[c][2] = i32x4{0, 0, 0, 0};
+            }
 #pragma unroll 1
             for (int ks = 0; ks < th.y; ++ks) {
                 i32x4 a[3];
 #pragma unroll
                 for (int q = 0; q < 3; ++q) a[q] = __builtin_bit_cast(i32x4, tblk[th.z + (ks * 3 + q) * 64 + lane]);
                 const int G = (th.x + 64 * ks + 16 * (lane >> 4)) >> 2;
-                const uint4* tq = reinterpret_cast<const uint4*>(tmp + v.src_off + (int64_t)G * v.src_pitch) + xs;
-                const uint4 g0 = tq[0], g1 = tq[gstride], g2 = tq[2 * gstride], g3 = tq[3 * gstride];
-                const i32x4 bq[4] = {i32x4{(int)g0.x, (int)g1.x, (int)g2.x, (int)g3.x},
-                                     i32x4{(int)g0.y, (int)g1.y, (int)g2.y, (int)g3.y},
-                                     i32x4{(int)g0.z, (int)g1.z, (int)g2.z, (int)g3.z},
-                                     i32x4{(int)g0.w, (int)g1.w, (int)g2.w, (int)g3.w}};
+                uint4 g[4];
+                if (SC1) {
+                    const uint32_t o0 = (uint32_t)(G * v.src_pitch + 16 * xs);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        g[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                             trs, o0 + (uint32_t)(j * v.src_pitch), 0, 16));
+                } else {
+                    const uint4* tq = reinterpret_cast<const uint4*>(tmp + v.src_off + (int64_t)G * v.src_pitch) + xs;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) g[j] = tq[j * gstride];
+                }
+                const i32x4 bq[4] = {i32x4{(int)g[0].x, (int)g[1].x, (int)g[2].x, (int)g[3].x},
+                                     i32x4{(int)g[0].y, (int)g[1].y, (int)g[2].y, (int)g[3].y},
+                                     i32x4{(int)g[0].z, (int)g[1].z, (int)g[2].z, (int)g[3].z},
+                                     i32x4{(int)g[0].w, (int)g[1].w, (int)g[2].w, (int)g[3].w}};
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -711,12 +804,11 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
                     const int row = 4 * (lane >> 4) + r;   // band row = tile row
                     const int o = y0 + row - p.y;           // overlay row
                     if (o >= oy_lo && o < oy_hi) {
-                        const int32_t bias = tbias[16 * t + row];
                         uint32_t px = 0;
 #pragma unroll
                         for (int c = 0; c < 4; ++c)
-                            px |= clip8(bias + acc[c][0][r] + (acc[c][1][r] << 8) + (acc[c][2][r] << 16)) << (8 * c);
-                        orow[row * ov_w_max + x] = unpremultiply(px);
+                            px |= clip8(acc[c][0][r] + (acc[c][1][r] << 8) + (acc[c][2][r] << 16)) << (8 * c);
+                        orow[row * os + xo + x] = (kVbX & 2) ? px : unpremultiply(px);
                     }
                 }
             }
@@ -725,11 +817,55 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
     }
 
     // Phase 2: composite rows = background bytes, blended inside the footprint.
-    // Four 16-B chunks per thread are loaded before any is stored, so each
-    // wave keeps four background reads in flight.
     const int row_bytes = 3 * p.bg_w;
+    const uint8_t* bgb = bg + p.bg_off + (int64_t)y0 * p.bg_pitch;
+    uint8_t* dsb = dst + p.dst_off + (int64_t)y0 * p.dst_pitch;
+    const bool groups = (p.bg_w & 15) == 0 && ((p.bg_pitch | p.dst_pitch) & 15) == 0 &&
+                        ((reinterpret_cast<uintptr_t>(bgb) | reinterpret_cast<uintptr_t>(dsb)) & 15u) == 0;
+    if (groups && !(DBG & 1) && !(kVbX & 4)) {
+        // 16-pixel groups: 48 bytes per thread and step (three 16-B loads in
+        // flight), the overlay pixels from orow, blended in 16-bit lanes.
+        const int G = p.bg_w >> 4, lg = 31 - __builtin_clz(G);
+        const bool pow2 = (G & (G - 1)) == 0;
+        const int total = nrows * G;
+        const int gx0 = p.x >> 4, gx1 = (p.x + p.ov_w + 15) >> 4;  // groups the overlay touches
+        for (int idx = threadIdx.x; idx < total; idx += 256) {
+            const int rr = pow2 ? idx >> lg : idx / G;
+            const int gi = idx - rr * G;
+            const uint4* sp = reinterpret_cast<const uint4*>(bgb + (int64_t)rr * p.bg_pitch) + 3 * gi;
+            uint32_t w[12];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const uint4 v4 = sp[q];
+                w[4 * q] = v4.x;
+                w[4 * q + 1] = v4.y;
+                w[4 * q + 2] = v4.z;
+                w[4 * q + 3] = v4.w;
+            }
+            const int o = y0 + rr - p.y;
+            if (!(kVbX & 1) && any && o >= oy_lo && o < oy_hi && gi >= gx0 && gi < gx1) {
+                const uint4* orw = reinterpret_cast<const uint4*>(orow + rr * os + 16 * (gi - gx0));
+                uint32_t ov[16];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint4 v4 = orw[q];
+                    ov[4 * q] = v4.x;
+                    ov[4 * q + 1] = v4.y;
+                    ov[4 * q + 2] = v4.z;
+                    ov[4 * q + 3] = v4.w;
+                }
+                blend48(w, ov);
+            }
+            uint8_t* dp = dsb + (int64_t)rr * p.dst_pitch + 48 * gi;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) store16<STORE>(dp + 16 * q, 16, true, w + 4 * q);
+        }
+        return;
+    }
+    // General layout: 16-B chunks, byte-wise blend.  Four chunks per thread are
+    // loaded before any is stored, so each wave keeps four reads in flight.
     const int chunks = (row_bytes + 15) >> 4;
-    const int total = nrows * chunks;
+    const int total = (kVbX & 4) ? 0 : nrows * chunks;
     for (int base = threadIdx.x; base < total; base += 4 * 256) {
         uint32_t w[4][4];
         int rr[4], c0[4], nb[4];
@@ -752,8 +888,8 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
         for (int u = 0; u < 4; ++u) {
             if (nb[u] <= 0) continue;
             const int o = y0 + rr[u] - p.y;
-            if (any && o >= oy_lo && o < oy_hi && c0[u] + nb[u] > 3 * p.x && c0[u] < 3 * (p.x + p.ov_w)) {
-                const uint32_t* orw = orow + rr[u] * ov_w_max;
+            if (!(kVbX & 1) && any && o >= oy_lo && o < oy_hi && c0[u] + nb[u] > 3 * p.x && c0[u] < 3 * (p.x + p.ov_w)) {
+                const uint32_t* orw = orow + rr[u] * os + xo;
                 blend16(w[u], c0[u], nb[u], p.x, p.ov_w, [&](int ox) { return orw[ox]; });
             }
             uint8_t* dp = dst + p.dst_off + (int64_t)(y0 + rr[u]) * p.dst_pitch + c0[u];
@@ -762,10 +898,126 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
     }
 }
 
+template <int STORE, int DBG = 0, bool BANDS = false>
+__global__ void __launch_bounds__(256)
+k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
+                   const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int tiles_y,
+                   int ov_w_max) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t orow[];  // [VBR][orow_stride(ov_w_max)]
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / tiles_y;
+    const int ty = b - im * tiles_y;
+    vblend_block<STORE, DBG, BANDS, false>(orow, tmp, bg, dst, coefs, descs, im, ty, ov_w_max);
+}
+
+// ---------------------------------------------------------------------------
+// Fused launch (ipp_pipe_fused): per item, its H-pass blocks, its background
+// copy blocks and — D items later in the block order — its V-pass bands, so
+// the latency-bound V pass runs beside the VALU-bound H pass.  A V block reads
+// the item's completion counter (agent scope) once: if every H block of the
+// item has finished it proceeds, reading T past the caches; otherwise it
+// queues its band and exits (no spinning: correctness does not depend on the
+// dispatch order or on the XCD a block lands on).  k_pipe_vdeferred then runs
+// the queued bands after the launch.
+//
+// Sync scratch (ipp_pipe_sync_bytes): int32 done[n]; int32 nq; int32 queue[n·tyv].
+// ---------------------------------------------------------------------------
+constexpr int FUSE_LAG = 4;  // items between an item's H blocks and its V bands
+
+template <int NR, bool ZONES, int CN>
+__global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES && NR > 8 ? 3 : 4)))
+k_pipe_fused(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
+             const ipp_pipe_desc* __restrict__ descs, int n, int tyb, int cpi, int tyv, ipp_hsv_params hp,
+             const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst, int ov_w_max, int32_t* __restrict__ sync) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t L = xcd_remap(blockIdx.x, gridDim.x);
+    const int A = tyb + cpi, U = A + tyv, D = min(FUSE_LAG, n);
+    // Block order: items 0..D-1 (H, copy); then per item i ≥ D: H(i), copy(i),
+    // V(i - D); then V(n - D .. n - 1).
+    int role, im, k;  // role 0: H / copy (k < tyb: H band k), 1: V band k
+    if (L < (uint32_t)(D * A)) {
+        role = 0;
+        im = L / A;
+        k = L - im * A;
+    } else if (L < (uint32_t)(D * A + (n - D) * U)) {
+        const int l = L - D * A;
+        const int q = l / U, r = l - q * U;
+        if (r < A) { role = 0; im = D + q; k = r; }
+        else { role = 1; im = q; k = r - A; }
+    } else {
+        const int l = L - D * A - (n - D) * U;
+        role = 1;
+        im = n - D + l / tyv;
+        k = l - (l / tyv) * tyv;
+    }
+    if (role == 0) {
+        if (k >= tyb) {
+            bg_copy_outside_bands<64 * HP_NW>(descs[im].p, bg, dst, k - tyb, cpi);
+            return;
+        }
+        hpass_block<NR, ZONES, CN, true>(*reinterpret_cast<Hpass2Lds<NR>*>(smem), src, tmp, coefs, descs, im, k, hp,
+                                         sync);
+        return;
+    }
+    {
+        // V band k of item im: nothing to do past the overlay bands
+        int vb0, vb1;
+        paste_bands(descs[im].p, vb0, vb1);
+        if (vb0 + VBR * k >= vb1) return;
+    }
+    __shared__ int32_t ready;
+    if (threadIdx.x == 0) {
+        const int need = (descs[im].h.lines + HR - 1) / HR;
+        const int got = __hip_atomic_load(sync + im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ready = got >= need;
+        if (!ready) {
+            const int slot = __hip_atomic_fetch_add(sync + n, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(sync + n + 1 + slot, im * tyv + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    if (!ready) return;
+    vblend_block<2, 0, true, true>(reinterpret_cast<uint32_t*>(smem), tmp, bg, dst, coefs, descs, im, k, ov_w_max);
+}
+
+// The bands queued by k_pipe_fused (after it: every H block has finished).
+__global__ void __launch_bounds__(256)
+k_pipe_vdeferred(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
+                 const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int n, int tyv,
+                 int ov_w_max, const int32_t* __restrict__ sync) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t orow[];
+    const int nq = sync[n];
+    for (int e = blockIdx.x; e < nq; e += gridDim.x) {
+        const int code = sync[n + 1 + e];
+        const int im = code / tyv, k = code - im * tyv;
+        vblend_block<2, 0, true, false>(orow, tmp, bg, dst, coefs, descs, im, k, ov_w_max);
+        __syncthreads();  // orow is reused by the next entry
+    }
+}
+
+// The fused launch's extra parameters (ipp_pipe_fused).
+struct FusedCfg {
+    int tyv, max_ov_w;
+    int32_t* sync;
+};
+
 template <int NR, bool ZONES, int CN>
 void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
-                  const ipp_pipe_desc* descs, int ty, const ipp_hsv_params& hp, const uint8_t* bg, uint8_t* dst) {
+                  const ipp_pipe_desc* descs, int ty, const ipp_hsv_params& hp, const uint8_t* bg, uint8_t* dst,
+                  const FusedCfg* fz) {
     const int n = grid.x / ty;
+    if (fz) {
+        const int cpi = copy_blocks_per_item();
+        const size_t vb = (size_t)VBR * orow_stride(fz->max_ov_w) * sizeof(uint32_t);
+        const size_t sm = std::max(sizeof(Hpass2Lds<NR>), vb);
+        if (hipMemsetAsync(fz->sync, 0, (size_t)(n + 1) * sizeof(int32_t), s) != hipSuccess) return;
+        hipLaunchKernelGGL((k_pipe_fused<NR, ZONES, CN>), dim3((uint32_t)(n * (ty + cpi + fz->tyv))),
+                           dim3(64 * HP_NW), sm, s, src, tmp, coefs, descs, n, ty, cpi, fz->tyv, hp, bg, dst,
+                           fz->max_ov_w, fz->sync);
+        hipLaunchKernelGGL(k_pipe_vdeferred, dim3((uint32_t)std::min(n * fz->tyv, 2048)), dim3(256), vb, s, tmp, bg,
+                           dst, coefs, descs, n, fz->tyv, fz->max_ov_w, fz->sync);
+        return;
+    }
     if (bg && dst) {  // H pass + the background rows outside the overlay bands
         const int cpi = copy_blocks_per_item();
         hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, true>), dim3((uint32_t)(n * (ty + cpi))), dim3(64 * HP_NW), 0,
@@ -779,13 +1031,13 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
 template <int NR>
 void launch_hpass_nr(bool zones, int cn, dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp,
                      const int32_t* coefs, const ipp_pipe_desc* descs, int ty, const ipp_hsv_params& hp,
-                     const uint8_t* bg, uint8_t* dst) {
+                     const uint8_t* bg, uint8_t* dst, const FusedCfg* fz) {
     if (zones) {
-        if (cn == 4) launch_hpass<NR, true, 4>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst);
-        else launch_hpass<NR, true, 3>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst);
+        if (cn == 4) launch_hpass<NR, true, 4>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst, fz);
+        else launch_hpass<NR, true, 3>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst, fz);
     } else {
-        if (cn == 4) launch_hpass<NR, false, 4>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst);
-        else launch_hpass<NR, false, 3>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst);
+        if (cn == 4) launch_hpass<NR, false, 4>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst, fz);
+        else launch_hpass<NR, false, 3>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst, fz);
     }
 }
 
@@ -794,14 +1046,14 @@ void launch_hpass_nr(bool zones, int cn, dim3 grid, hipStream_t s, const uint8_t
 static int pipe_hpass_impl(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
                            int32_t n_images, int32_t max_out_w, int32_t max_rows, int32_t src_cn,
                            const ipp_hsv_params* hsv, int32_t tap_format, const uint8_t* bg, uint8_t* dst,
-                           void* stream) {
+                           void* stream, const FusedCfg* fz = nullptr) {
     if (n_images == 0) return IPP_OK;
     if (!src || !tmp || !coefs || !descs || !hsv || n_images < 0 || max_out_w <= 0 || max_rows <= 0) return IPP_E_ARG;
     if (src_cn != 3 && src_cn != 4) return IPP_E_ARG;
     if (tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;  // the VALU dot4 kernels were retired
     const int ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
     const int64_t blocks = (int64_t)ty * n_images;
-    if ((int64_t)(ty + (bg ? copy_blocks_per_item() : 0)) * n_images >= INT32_MAX) return IPP_E_ARG;
+    if ((int64_t)(ty + (bg ? copy_blocks_per_item() : 0) + (fz ? fz->tyv : 0)) * n_images >= INT32_MAX) return IPP_E_ARG;
     const dim3 grid((uint32_t)blocks);
     hipStream_t s = (hipStream_t)stream;
     // Zones are needed unless every range's zone is the whole image (all
@@ -813,21 +1065,21 @@ static int pipe_hpass_impl(const uint8_t* src, uint8_t* tmp, const int32_t* coef
     // A range that never matches: lo_v = 1 > hi_v = 0 (cv::inRange's empty range).
     const ipp_hsv_range never = ipp_hsv_range{{0, 0, 1}, {180, 255, 0}, {0, 0, 0, 0}};
     switch (hsv->n_ranges) {
-        case 1: launch_hpass_nr<1>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst); break;
-        case 2: launch_hpass_nr<2>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst); break;
-        case 3: launch_hpass_nr<3>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst); break;
-        case 4: launch_hpass_nr<4>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst); break;
+        case 1: launch_hpass_nr<1>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst, fz); break;
+        case 2: launch_hpass_nr<2>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst, fz); break;
+        case 3: launch_hpass_nr<3>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst, fz); break;
+        case 4: launch_hpass_nr<4>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst, fz); break;
         case 5: case 6: {
             ipp_hsv_params q = *hsv;  // pad with never-matching ranges (lo > hi in v)
             for (int k = q.n_ranges; k < 6; ++k) q.r[k] = never;
-            launch_hpass_nr<6>(zones, cn, grid, s, src, tmp, coefs, descs, ty, q, bg, dst);
+            launch_hpass_nr<6>(zones, cn, grid, s, src, tmp, coefs, descs, ty, q, bg, dst, fz);
             break;
         }
         default: {
             if (hsv->n_ranges > IPP_MAX_HSV_RANGES) return IPP_E_ARG;
             ipp_hsv_params q = *hsv;
             for (int k = q.n_ranges; k < IPP_MAX_HSV_RANGES; ++k) q.r[k] = never;
-            launch_hpass_nr<IPP_MAX_HSV_RANGES>(zones, cn, grid, s, src, tmp, coefs, descs, ty, q, bg, dst);
+            launch_hpass_nr<IPP_MAX_HSV_RANGES>(zones, cn, grid, s, src, tmp, coefs, descs, ty, q, bg, dst, fz);
             break;
         }
     }
@@ -852,6 +1104,31 @@ extern "C" int ipp_pipe_hpass_bgcopy(const uint8_t* src, uint8_t* tmp, const int
                            stream);
 }
 
+// Bands per item of the fused launch: an overlay of height H at any y spans
+// at most ceil((15 + H) / 16) 16-row bands.
+static int fused_tyv(int32_t bg_h, int32_t max_ov_h) {
+    return std::min((max_ov_h + 15 + VBR - 1) / VBR, (bg_h + VBR - 1) / VBR);
+}
+
+extern "C" int64_t ipp_pipe_sync_bytes(int32_t n_images, int32_t bg_h, int32_t max_ov_h) {
+    if (n_images < 0 || bg_h <= 0 || max_ov_h <= 0) return -1;
+    return (int64_t)sizeof(int32_t) * (1 + n_images + (int64_t)n_images * fused_tyv(bg_h, max_ov_h));
+}
+
+extern "C" int ipp_pipe_fused(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
+                              int32_t n_images, int32_t max_out_w, int32_t max_rows, int32_t src_cn,
+                              const ipp_hsv_params* hsv, int32_t tap_format, const uint8_t* bg, uint8_t* dst,
+                              int32_t bg_w, int32_t bg_h, int32_t max_ov_w, int32_t max_ov_h, void* sync,
+                              void* stream) {
+    if (n_images == 0) return IPP_OK;
+    if (!bg || !dst || !sync || tap_format != IPP_TAPS_MFMA || bg_w <= 0 || bg_h <= 0) return IPP_E_ARG;
+    if (max_ov_w <= 0 || max_ov_w > bg_w || max_ov_h <= 0 || max_ov_h > bg_h) return IPP_E_ARG;
+    if ((size_t)VBR * orow_stride(max_ov_w) * sizeof(uint32_t) > 64 * 1024) return IPP_E_ARG;
+    const FusedCfg fz{fused_tyv(bg_h, max_ov_h), max_ov_w, reinterpret_cast<int32_t*>(sync)};
+    return pipe_hpass_impl(src, tmp, coefs, descs, n_images, max_out_w, max_rows, src_cn, hsv, tap_format, bg, dst,
+                           stream, &fz);
+}
+
 extern "C" int ipp_pipe_status(int32_t* status, void* stream) {
     if (!status) return IPP_E_ARG;
     hipStream_t s = (hipStream_t)stream;
@@ -872,7 +1149,7 @@ extern "C" int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint
     if (!tmp || !bg || !dst || !coefs || !descs || n_images < 0 || bg_w <= 0 || bg_h <= 0) return IPP_E_ARG;
     if (tap_format != IPP_TAPS_MFMA || max_ov_w <= 0 || max_ov_w > bg_w || max_ov_h <= 0 || max_ov_h > bg_h)
         return IPP_E_ARG;
-    const size_t sm = (size_t)VBR * max_ov_w * sizeof(uint32_t);
+    const size_t sm = (size_t)VBR * orow_stride(max_ov_w) * sizeof(uint32_t);
     // an overlay of height H at any y spans at most ceil((15 + H) / 16) bands
     const int tyb = std::min((max_ov_h + 15 + VBR - 1) / VBR, (bg_h + VBR - 1) / VBR);
     const int64_t nb = (int64_t)tyb * n_images;
@@ -889,7 +1166,7 @@ extern "C" int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* d
     if (n_images == 0) return IPP_OK;
     if (!tmp || !bg || !dst || !coefs || !descs || n_images < 0 || bg_w <= 0 || bg_h <= 0) return IPP_E_ARG;
     if (tap_format != IPP_TAPS_MFMA || max_ov_w <= 0 || max_ov_w > bg_w) return IPP_E_ARG;
-    const size_t sm = (size_t)VBR * max_ov_w * sizeof(uint32_t);
+    const size_t sm = (size_t)VBR * orow_stride(max_ov_w) * sizeof(uint32_t);
     const int tyb = (bg_h + VBR - 1) / VBR;
     const int64_t nb = (int64_t)tyb * n_images;
     if (nb >= INT32_MAX || sm > 64 * 1024) return IPP_E_ARG;

@@ -46,49 +46,68 @@ class CclScratch:
         self.bbox = torch.empty(4 * n, dtype=torch.int32, device=device)
 
 
-def keep_largest_masks(imgs: Sequence[torch.Tensor]) -> List[Optional[Tuple[int, int, int, int]]]:
-    """In place on each (H, W, 4) image: α zeroed outside the largest
-    component.  Returns the α ≠ 0 bbox (x0, y0, x1, y1) per image or None."""
-    if not imgs:
+def keep_largest_packed(buf: torch.Tensor, offs: Sequence[int],
+                        dims: Sequence[Tuple[int, int]]) -> List[Optional[Tuple[int, int, int, int]]]:
+    """In place on (H, W, 4) images packed in one contiguous device byte
+    buffer at byte offsets `offs` (dims = (H, W) each): α zeroed outside the
+    largest component.  Returns the α ≠ 0 bbox (x0, y0, x1, y1) per image or
+    None (no pixel left)."""
+    if not dims:
         return []
-    dev = imgs[0].device
-    n = len(imgs)
+    _require_cuda(buf, "keep_largest_component")
+    if buf.dtype != torch.uint8 or not buf.is_contiguous():
+        raise ValueError("keep_largest_packed expects a contiguous uint8 buffer")
+    dev = buf.device
+    n = len(dims)
     d = np.zeros(n, N.IMAGE_DESC)
-    off = 0
-    flat = []
-    for i, im in enumerate(imgs):
-        _require_cuda(im, "keep_largest_component")
-        if im.dim() != 3 or im.shape[2] != 4:
-            raise ValueError("keep_largest_component expects (H, W, 4) images")
-        h, w, _ = im.shape
+    for i, ((h, w), off) in enumerate(zip(dims, offs)):
+        if off < 0 or off + 4 * h * w > buf.numel():
+            raise ValueError(f"image {i} ({h}x{w}x4 at {off}) outside the buffer")
         d[i]["off"], d[i]["w"], d[i]["h"], d[i]["pitch"], d[i]["cn"] = off, w, h, 4 * w, 4
-        off += h * w * 4
-        flat.append(im.contiguous().reshape(-1))
-    buf = torch.cat(flat) if n > 1 else flat[0]
-    sc = CclScratch([(int(im.shape[0]), int(im.shape[1])) for im in imgs], dev)
-    mw = max(int(im.shape[1]) for im in imgs)
-    mh = max(int(im.shape[0]) for im in imgs)
+    sc = CclScratch([(int(h), int(w)) for h, w in dims], dev)
+    mw = max(int(w) for _, w in dims)
+    mh = max(int(h) for h, _ in dims)
     dd = _to_dev(d, dev)
     N.check(N.load().ipp_ccl_keep_largest(buf.data_ptr(), dd.data_ptr(), n, mw, mh, sc.works_dev.data_ptr(),
                                           sc.scratch.data_ptr(), sc.max_ent, sc.counts.data_ptr(),
                                           sc.stats.data_ptr(), sc.bbox.data_ptr(), _stream(dev)),
             "ipp_ccl_keep_largest")
     _keep(dd)
-    off = 0
-    for im in imgs:  # write back when the inputs were not contiguous views of buf
-        sz = im.numel()
-        if n > 1 or not im.is_contiguous() or im.data_ptr() != buf.data_ptr():
-            im.copy_(buf[off:off + sz].view(im.shape))
-        off += sz
     bb = sc.bbox.cpu().numpy().reshape(n, 4)
     out: List[Optional[Tuple[int, int, int, int]]] = []
     for i, r in enumerate(bb):
         if r[0] >= 0:
             out.append(tuple(int(v) for v in r))
         else:
-            # no component: α was left unchanged (label 0 kept) — crop to its α ≠ 0 pixels
-            out.append(alpha_bbox([imgs[i]])[0])
+            # no component (no α > 1): label 0 is kept and α left unchanged
+            # (pixels_isolés.py:38-47) — crop to its α ≠ 0 pixels (:77-81)
+            h, w = dims[i]
+            out.append(alpha_bbox([buf[offs[i]:offs[i] + 4 * h * w].view(h, w, 4)])[0])
     return out
+
+
+def keep_largest_masks(imgs: Sequence[torch.Tensor]) -> List[Optional[Tuple[int, int, int, int]]]:
+    """In place on each (H, W, 4) image: α zeroed outside the largest
+    component.  Returns the α ≠ 0 bbox (x0, y0, x1, y1) per image or None."""
+    if not imgs:
+        return []
+    for im in imgs:
+        _require_cuda(im, "keep_largest_component")
+        if im.dim() != 3 or im.shape[2] != 4:
+            raise ValueError("keep_largest_component expects (H, W, 4) images")
+    n = len(imgs)
+    if n == 1 and imgs[0].is_contiguous() and imgs[0].dtype == torch.uint8:
+        im = imgs[0]
+        return keep_largest_packed(im.view(-1), [0], [(int(im.shape[0]), int(im.shape[1]))])
+    offs, off = [], 0
+    for im in imgs:
+        offs.append(off)
+        off += im.numel()
+    buf = torch.cat([im.contiguous().reshape(-1) for im in imgs])
+    res = keep_largest_packed(buf, offs, [(int(im.shape[0]), int(im.shape[1])) for im in imgs])
+    for im, o in zip(imgs, offs):
+        im.copy_(buf[o:o + im.numel()].view(im.shape))
+    return res
 
 
 def keep_largest_component(img: torch.Tensor) -> torch.Tensor:

@@ -313,6 +313,10 @@ class PipeRunner:
         self.coefs = torch.from_numpy(plan.coefs).to(self.device)
         self.tmp = torch.empty(plan.tmp_bytes, dtype=torch.uint8, device=self.device)
         self.lib = N.load()
+        nb = self.lib.ipp_pipe_sync_bytes(len(plan.descs), plan.bg_h, plan.max_ov_h)
+        if nb < 0:
+            raise N.NativeError(f"ipp_pipe_sync_bytes({len(plan.descs)}, {plan.bg_h}, {plan.max_ov_h}) failed")
+        self.sync = torch.empty(max(int(nb), 4), dtype=torch.uint8, device=self.device)
 
     def hpass(self, src: torch.Tensor) -> None:
         p = self.plan
@@ -342,6 +346,22 @@ class PipeRunner:
                                                p.bg_h, p.max_ov_w, p.max_ov_h, p.tap_format,
                                                _stream(self.device)), "ipp_pipe_vblend_bands")
 
+    def fused(self, src: torch.Tensor, bgs: torch.Tensor, out: torch.Tensor) -> None:
+        """The whole pipe in one launch (+ the queued-band launch): H pass,
+        background copy and V pass with paste (ipp_pipe_fused)."""
+        p = self.plan
+        N.check(self.lib.ipp_pipe_fused(src.data_ptr(), self.tmp.data_ptr(), self.coefs.data_ptr(),
+                                        self.descs.data_ptr(), len(p.descs), p.max_out_w, p.max_rows, 3,
+                                        N.np_ptr(p.hsv), p.tap_format, bgs.data_ptr(), out.data_ptr(), p.bg_w,
+                                        p.bg_h, p.max_ov_w, p.max_ov_h, self.sync.data_ptr(),
+                                        _stream(self.device)), "ipp_pipe_fused")
+
+    def queued_bands(self) -> int:
+        """Bands the last fused launch queued for its second launch (not
+        ready when their block started).  Synchronises."""
+        torch.cuda.synchronize(self.device)
+        return int(self.sync[4 * len(self.plan.descs):4 * len(self.plan.descs) + 4].view(torch.int32).item())
+
     def status(self) -> int:
         """Sticky status of the pipe kernels since the last call (ipp_pipe_status;
         bit 0: an H tile's window exceeded the LDS ring).  Synchronises."""
@@ -358,8 +378,7 @@ class PipeRunner:
             if not (t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous()):
                 raise N.NativeUnavailable(f"PipeRunner.run: {name} must be a contiguous uint8 ROCm tensor")
         if self.split:
-            self.hpass_bgcopy(src, bgs, out)
-            self.vblend_bands(bgs, out)
+            self.fused(src, bgs, out)
         else:
             self.hpass(src)
             self.vblend(bgs, out)

@@ -33,9 +33,17 @@ def imread(path, flags: int = IMREAD_COLOR) -> Optional[np.ndarray]:
     tag (camera JPEGs come out upright, so crop_square's YOLO boxes land on
     the right pixels) and IMREAD_UNCHANGED does not.  IMREAD_UNCHANGED keeps
     16-bit single-channel images as uint16 (and 32-bit float ones as
-    float32), as cv2 does; other deep modes are refused (None)."""
+    float32), as cv2 does; other deep modes are refused (None) — among them
+    16-bit colour PNGs, which Pillow would silently decode to 8 bits where
+    cv2.IMREAD_UNCHANGED keeps 16 (their raw mode is 'RGB;16B' /
+    'RGBA;16B').  IMREAD_COLOR / IMREAD_GRAYSCALE reduce them to 8 bits (the
+    high byte), as cv2 does."""
     try:
         with Image.open(str(path)) as im:
+            if flags == IMREAD_UNCHANGED and not str(im.mode).startswith("I;16") and any(
+                    str(t[3][0] if isinstance(t[3], tuple) else t[3]).endswith(";16B")
+                    for t in getattr(im, "tile", []) or []):
+                return None
             im.load()
             mode = im.mode
             if flags == IMREAD_UNCHANGED:

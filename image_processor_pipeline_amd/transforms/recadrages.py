@@ -107,15 +107,38 @@ def fit_crop(image_path: Path, output_dirs: List[Path], **options: Any) -> Optio
     """Crop to Pillow's getbbox() (recadrages.py:63-82)."""
     output_dir = Path(output_dirs[0])
     image = Image.open(image_path)
+    image.load()
     arr = np.asarray(image)
-    t = _rt.h2d(arr)
-    bb = D.alpha_bbox([t])[0]
+    if arr.dtype == bool:                      # mode '1'
+        arr = arr.astype(np.uint8)
+    h, w = arr.shape[:2]
+    px = np.ascontiguousarray(arr).view(np.uint8).reshape(h, w, -1)   # bytes per pixel
+    bpp = px.shape[2]
+    t = _rt.h2d(px)
+    # Pillow getbbox(alpha_only=True): the alpha band when the mode has one,
+    # else every band (CMYK, RGBX, RGB, L, I;16, …) — non-zero bytes of a
+    # pixel are a non-zero pixel.
+    if image.mode in ("RGBA", "LA", "PA", "RGBa", "La"):
+        bb = D.alpha_bbox([t])[0]
+    else:
+        bb = D.alpha_bbox([t.view(h, w * bpp, 1)])[0]
+        if bb:
+            bb = (bb[0] // bpp, bb[1], (bb[2] - 1) // bpp + 1, bb[3])
     if not bb:
         new_image = image.copy()
     else:
         x0, y0, x1, y1 = bb
         out = _rt.d2h(D.copy_window(t, (x0, y0, x1 - x0, y1 - y0)))
-        new_image = Image.fromarray(out[..., 0] if arr.ndim == 2 else out, image.mode)
+        out = np.ascontiguousarray(out).view(arr.dtype).reshape((y1 - y0, x1 - x0) + arr.shape[2:])
+        if image.mode == "1":
+            new_image = Image.fromarray(out.astype(bool))
+        elif arr.ndim == 2 and image.mode != "P":
+            new_image = Image.fromarray(out)            # L, I;16, I, F
+        else:
+            new_image = Image.fromarray(out, image.mode)
+        if image.mode == "P":
+            new_image.putpalette(image.getpalette())
+            new_image.info = dict(image.info)
     output_path = output_dir / image_path.name
     new_image.save(output_path)
     return output_path

@@ -98,7 +98,7 @@ def _symmetries_batch(arg_tuples, output_dirs: List[Path], threads: int = 1, poo
                                     include_original=include_original, **options) for a in arg_tuples]
     output_dir = Path(output_dirs[0])
 
-    def load(args):
+    def validate(args):
         input_path = args[0]
         if input_path.suffix.lower()[1:] not in _io.IMG_FORMATS:
             raise ValueError(f"Le fichier {input_path.name} n'est pas un format accepté par Yolo.")
@@ -111,6 +111,23 @@ def _symmetries_batch(arg_tuples, output_dirs: List[Path], threads: int = 1, poo
         elif k < 0:
             raise ValueError(f"[{input_path.name} - Symétrie] `choose_random` ({k}) doit être >= 0. "
                              "Aucune symétrie aléatoire générée.")
+        return pl, k
+
+    # The checks (and their warnings) run here, on this thread, in file order
+    # — as the per-file calls would emit them; only decoding goes to threads.
+    checked = {}
+    for a in arg_tuples:
+        try:
+            checked[id(a)] = validate(a)
+        except Exception as e:
+            checked[id(a)] = e
+
+    def load(args):
+        input_path = args[0]
+        c = checked[id(args)]
+        if isinstance(c, Exception):
+            raise c
+        pl, k = c
         image = _io.imread(str(input_path), _io.IMREAD_UNCHANGED)
         if image is None:
             raise FileNotFoundError(f"[{input_path.name} - Symétrie] Impossible de charger l'image.")

@@ -252,6 +252,26 @@ int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
                           int32_t bg_w, int32_t bg_h, int32_t max_ov_w, int32_t max_ov_h,
                           int32_t tap_format, void* stream);
 
+/* One-launch form of the split pair (the default of fused.PipeRunner.run and
+ * of bench.py; same reference call sites: rotations.py:96, filtres_liste.py:
+ * 84-134, overlays.py:129,138-139).  The V-pass bands of item i run inside the
+ * H-pass launch, placed a few items after i's H blocks, so the latency-bound V
+ * pass overlaps the VALU-bound H pass.  A V band starts only if every H block
+ * of its item has finished (a per-item counter in `sync`; T is handed over
+ * with write-through stores and cache-bypassing loads); otherwise it is queued
+ * and a second launch, issued by this call, runs the queue.  No block waits
+ * for another, so correctness does not depend on the dispatch order.
+ * sync: device scratch of ipp_pipe_sync_bytes(n_images, bg_h, max_ov_h) bytes
+ * (its counters are reset by this call, on `stream`).  Writes exactly what
+ * ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands write. */
+int64_t ipp_pipe_sync_bytes(int32_t n_images, int32_t bg_h, int32_t max_ov_h);
+int ipp_pipe_fused(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
+                   const ipp_pipe_desc* descs, int32_t n_images,
+                   int32_t max_out_w, int32_t max_rows, int32_t src_cn,
+                   const ipp_hsv_params* hsv, int32_t tap_format,
+                   const uint8_t* bg, uint8_t* dst, int32_t bg_w, int32_t bg_h,
+                   int32_t max_ov_w, int32_t max_ov_h, void* sync, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* K10-K13: pixels_isolés.keep_largest_component                             */
 /* :32 threshold(α,1,255) :35 connectedComponentsWithStats(8) :38-55 keep    */

@@ -57,3 +57,26 @@ def sha256(a) -> str:
 # HSV exclusion range that never matches (OpenCV 8-bit hue < 180): α = 255
 # everywhere, so the pipe chain is Pillow-only (pipe_config3_pillow.npz).
 NEVER_RANGE = (180, 0, 0, 180, 255, 255)
+
+
+# HSV exclusion range holding exactly the pure-black pixels (V = max(r, g, b)
+# = 0): the α = 0 path of the pipe pinned by Pillow alone
+# (pipe_config3_black_pillow.npz, tools/make_goldens.py).
+BLACK_RANGE = (0, 0, 0, 180, 255, 0)
+CONFIG3_BLACK_SEED = 5000
+
+
+def config3_black_source(i: int) -> np.ndarray:
+    """Item i's 1024² source for pipe_config3_black_pillow.npz: random bytes
+    with planted black (0, 0, 0) rectangles, stripes and 3 % scattered black
+    pixels, so the cut-out has α = 0 regions of every size."""
+    src = np.random.default_rng(CONFIG3_BLACK_SEED + i).integers(0, 256, (1024, 1024, 3), np.uint8)
+    r = np.random.default_rng(CONFIG3_BLACK_SEED + 100 + i)
+    for _ in range(8):
+        y0, x0 = (int(v) for v in r.integers(0, 1000, 2))
+        hh, ww = (int(v) for v in r.integers(8, 260, 2))
+        src[y0:y0 + hh, x0:x0 + ww] = 0
+    src[:, 300 + 37 * i:304 + 37 * i] = 0
+    src[500 + 11 * i:503 + 11 * i, :] = 0
+    src[r.random((1024, 1024)) < 0.03] = 0
+    return src

@@ -266,6 +266,38 @@ def test_pipe_split_equals_unsplit(D):
             assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (bw, i)
 
 
+def test_pipe_fused_equals_split(D):
+    """ipp_pipe_fused (H pass, copy and V bands in one launch, a per-item
+    completion counter, queued bands in a second launch) writes exactly what
+    the two-launch split form writes, for batches small enough that bands are
+    queued (the V blocks of the last items follow their H blocks at once) and
+    larger ones; odd background widths take the row-wise copy path."""
+    from image_processor_pipeline_amd import fused
+    cfg = fused.PipeConfig(margins=(3, 5, 2, 7), scale_min=0.2, scale_max=0.7)
+    queued = 0
+    for (n, bh, bw) in [(1, 97, 125), (3, 64, 96), (40, 120, 160)]:
+        H, W = 90, 110
+        rng = np.random.default_rng(n)
+        src = rng.integers(0, 256, (n, H, W, 3), np.uint8)
+        bgs = rng.integers(0, 256, (3, bh, bw, 3), np.uint8)
+        plan = fused.plan_pipe((H, W), n, (bh, bw), 3, cfg, seed=n)
+        runner = fused.PipeRunner(plan, DEV)
+        a = torch.full((n, bh, bw, 3), 7, dtype=torch.uint8, device=DEV)
+        b = torch.full((n, bh, bw, 3), 9, dtype=torch.uint8, device=DEV)
+        for _ in range(2):  # the second run reuses T and the counters
+            runner.fused(_t(src), _t(bgs), a)
+            queued += runner.queued_bands()
+        runner.hpass_bgcopy(_t(src), _t(bgs), b)
+        runner.vblend_bands(_t(bgs), b)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), n
+        assert runner.status() == 0
+        got = a.cpu().numpy()
+        for i in range(n):
+            assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (n, i)
+    print("bands queued for the second launch:", queued)
+
+
 def test_pipe_crop_reaching_source_end(D):
     """Zero bottom/right margins: the crop window ends at the source's last
     byte, so the last pixel's 4-byte gather would cross the image (and, for
@@ -526,6 +558,30 @@ def test_rotate_bilinear_large_vs_oracle(D):
     for a in (12.5, 45.0, 200.3):
         got = D.rotate_crop_bilinear(_t(img), a).cpu().numpy()
         assert np.array_equal(got, ops.rotate_and_crop(img, a, "bilinear")), a
+
+
+@pytest.mark.parametrize("i", range(6))
+def test_pipe_config3_alpha_zero_matches_pillow(D, golden, i):
+    """The fused pipe's α = 0 path at config-3 geometry against Pillow alone
+    (pipe_config3_black_pillow.npz): black planted in the 1024² source, the
+    one exclusion range holding exactly the black pixels (fill included), so
+    the cut-out has α = 0 regions of every size and the overlay partial α."""
+    from image_processor_pipeline_amd import fused
+    from tests.conftest import BLACK_RANGE, config3_black_source, sha256
+    g = golden("pipe_config3_black_pillow.npz")
+    src = config3_black_source(i)
+    bgs = np.stack([np.random.default_rng(int(g["bg_seed"]) + k).integers(0, 256, (1024, 1024, 3), np.uint8)
+                    for k in range(2)])
+    x, y = (int(v) for v in g["xy"][i])
+    cfg = fused.PipeConfig(hsv_ranges=[BLACK_RANGE])
+    plan = fused.plan_pipe((1024, 1024), 1, (1024, 1024), 2, cfg,
+                           params=[fused.ItemParams(float(g["angles"][i]), str(g["syms"][i]), int(g["bg_index"][i]),
+                                                    float(g["ratios"][i]), x, y)])
+    assert plan.ov_dims[0] == tuple(int(v) for v in g["ov_wh"][i])[::-1]
+    runner = fused.PipeRunner(plan, DEV)
+    out = torch.empty((1, 1024, 1024, 3), dtype=torch.uint8, device=DEV)
+    runner.run(_t(src[None]), _t(bgs), out)
+    assert sha256(out[0].cpu().numpy()) == str(g["comp_sha"][i])
 
 
 @pytest.mark.parametrize("i", range(6))

@@ -104,6 +104,27 @@ def test_oracle_pipe_at_config3_geometry_matches_pillow(golden, i):
     assert sha256(ops.paste_rgba_onto_rgb(bgs[bgi], ovr, x, y)) == str(g["comp_sha"][i])
 
 
+@pytest.mark.parametrize("i", [1, 4])
+def test_oracle_pipe_alpha_zero_matches_pillow(golden, i):
+    """The α = 0 path at config-3 geometry (pipe_config3_black_pillow.npz):
+    black planted in the source and the exclusion range that holds exactly
+    the black pixels, so the oracle's own HSV mask, LANCZOS over premultiplied
+    α = 0 pixels, unpremultiply and paste are pinned by Pillow alone."""
+    from image_processor_pipeline_amd import fused
+    from oracle import pipe as opipe
+    from tests.conftest import BLACK_RANGE, config3_black_source, sha256
+    g = golden("pipe_config3_black_pillow.npz")
+    assert int(g["alpha_zero"][i]) > 1000 and int(g["alpha_partial"][i]) > 1000
+    src = config3_black_source(i)
+    bgs = np.stack([np.random.default_rng(int(g["bg_seed"]) + k).integers(0, 256, (1024, 1024, 3), np.uint8)
+                    for k in range(2)])
+    x, y = (int(v) for v in g["xy"][i])
+    cfg = fused.PipeConfig(hsv_ranges=[BLACK_RANGE])
+    p = fused.ItemParams(float(g["angles"][i]), str(g["syms"][i]), int(g["bg_index"][i]), float(g["ratios"][i]),
+                         x, y)
+    assert sha256(opipe.pipe_item(src, bgs, p, cfg)) == str(g["comp_sha"][i])
+
+
 def test_enhance_image_reference_outputs(golden):
     """tranfo.enhance_image: the oracle (Blend.c / rgb2l / ImageStat /
     BoxBlur.c / point() restated) with the draws taken in the reference order

@@ -12,5 +12,5 @@ for name in "$@"; do
   IPP_LIB_PATH=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py $ARGS > $OUT/kt.log 2>&1 || exit 11
   find $OUT/kt -name '*kernel_trace.csv' -delete
   IPP_LIB_PATH=$lib timeout -k 10 300 rocprofv3 --kernel-include-regex 'k_pipe' --pmc $CNT --output-format csv -d $OUT/pmc -o pmc -- python3 bench.py $ARGS > $OUT/pmc.log 2>&1 || exit 12
-  echo "== $name"; python3 tools/prof_summary.py $OUT | grep hpass
+  echo "== $name"; python3 tools/prof_summary.py $OUT | grep -E "${PAT:-hpass}"
 done
