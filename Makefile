@@ -6,11 +6,11 @@ PKG := image_processor_pipeline_amd
 CSRC := $(PKG)/csrc
 SRCS := $(CSRC)/ipp_gather.hip $(CSRC)/ipp_hsv.hip $(CSRC)/ipp_resample.hip $(CSRC)/ipp_pipe.hip \
         $(CSRC)/ipp_ccl.hip $(CSRC)/ipp_util.hip $(CSRC)/ipp_bilinear.hip \
-        $(CSRC)/ipp_enhance.hip
-HOST_SRCS := $(CSRC)/ipp_host.cpp
+        $(CSRC)/ipp_enhance.hip $(CSRC)/ipp_taps.hip
+HOST_SRCS := $(CSRC)/ipp_host.cpp $(CSRC)/ipp_plan.cpp
 HDRS := include/ipp.h $(wildcard $(CSRC)/*.h)
 OBJDIR := build/obj
-OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS)) $(OBJDIR)/ipp_host.o
+OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS)) $(OBJDIR)/ipp_host.o $(OBJDIR)/ipp_plan.o
 LIB := $(PKG)/libipp.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 HOSTFLAGS := -O2 -std=c++17 -fPIC -Iinclude
@@ -22,15 +22,16 @@ all: $(LIB) $(OBJDIR)/ipp_pipe.s
 $(OBJDIR)/ipp_pipe.s: $(CSRC)/ipp_pipe.hip $(HDRS) | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -S --cuda-device-only $< -o $@
 
-# Pillow's BILINEAR (double) and Blend (float) arithmetic is plain mul/add
-# (x86-64 baseline, no FMA): these files must not contract a*b+c into fma,
-# inlined HIP header helpers included.
-$(OBJDIR)/ipp_bilinear.o $(OBJDIR)/ipp_enhance.o: HIPFLAGS += -ffp-contract=off
+# Pillow's BILINEAR (double), Blend (float) and LANCZOS tap (double)
+# arithmetic is plain mul/add (x86-64 baseline, no FMA): these files must not
+# contract a*b+c into fma, inlined HIP header helpers included.
+FPEXACT := ipp_bilinear.hip ipp_enhance.hip ipp_taps.hip
+$(OBJDIR)/ipp_bilinear.o $(OBJDIR)/ipp_enhance.o $(OBJDIR)/ipp_taps.o: HIPFLAGS += -ffp-contract=off
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS) | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/ipp_host.o: $(CSRC)/ipp_host.cpp $(HDRS) | $(OBJDIR)
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS) | $(OBJDIR)
 	g++ $(HOSTFLAGS) -c $< -o $@
 
 $(OBJDIR):
@@ -44,11 +45,11 @@ asm: | $(OBJDIR)
 
 # Experiment builds (A/B on the GPU box through IPP_LIB_PATH): one in-tree
 # library per variant, variants/<name>/libipp.so, built with VFLAGS.
-#   make variant NAME=fill VFLAGS=-DIPP_HP_FILL_SKIP
+#   make variant NAME=wpe6 VFLAGS=-DIPP_CCL_WPE=6
 variant:
 	mkdir -p variants/$(NAME)/obj
-	for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) $(VFLAGS) $$( [ "$$(basename $$f)" = ipp_bilinear.hip -o "$$(basename $$f)" = ipp_enhance.hip ] && echo -ffp-contract=off ) -c $$f -o variants/$(NAME)/obj/$$(basename $$f .hip).o || exit 1; done
-	g++ $(HOSTFLAGS) -c $(CSRC)/ipp_host.cpp -o variants/$(NAME)/obj/ipp_host.o
+	for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) $(VFLAGS) $$(echo " $(FPEXACT) " | grep -q " $$(basename $$f) " && echo -ffp-contract=off) -c $$f -o variants/$(NAME)/obj/$$(basename $$f .hip).o || exit 1; done
+	for f in $(HOST_SRCS); do g++ $(HOSTFLAGS) -c $$f -o variants/$(NAME)/obj/$$(basename $$f .cpp).o || exit 1; done
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o variants/$(NAME)/libipp.so variants/$(NAME)/obj/*.o -lpthread
 
 clean:

@@ -64,6 +64,9 @@ def parse(argv=None):
     ap.add_argument("--unsplit", action="store_true", help="pipe5: ipp_pipe_hpass + full-frame ipp_pipe_vblend")
     ap.add_argument("--split", action="store_true",
                     help="pipe5: ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands (two launches) instead of ipp_pipe_fused")
+    ap.add_argument("--stream", action="store_true",
+                    help="pipe5: also run the streaming form (a new plan per batch, planned on a host thread "
+                         "while the previous batch runs) and report it beside the resident step")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: CPU rehearsal of the N-rank path (tests)")
     ap.add_argument("--dump-digests", default=None,
@@ -263,6 +266,7 @@ def main(argv=None):
     fused_bound = None
 
     t_plan = time.perf_counter()
+    setup = {}
     if args.workload == "pipe5":
         src = make_sources(start, stop, S, args.seed, dev)
         bgs = torch.empty((K, S, S, 3), dtype=torch.uint8, device=dev)
@@ -272,8 +276,18 @@ def main(argv=None):
             bgs.copy_(torch.randint(0, 256, (K, S, S, 3), dtype=torch.uint8, device=dev, generator=g0))
         broadcast(bgs, world, args.dist_backend)
         cfg = fused.PipeConfig()
-        plan = fused.plan_pipe((S, S), B, (S, S), K, cfg, seed=args.seed * 7919, item_range=(start, stop),
-                               n_global=n_global)
+        if torch.device(dev).type == "cuda":
+            torch.cuda.synchronize(dev)
+        t_src = time.perf_counter()
+        setup["sources_ms"] = round((t_src - t_plan) * 1e3, 1)
+
+        def plan_batch(k):
+            return fused.plan_pipe((S, S), B, (S, S), K, cfg, seed=args.seed * 7919 + k, item_range=(start, stop),
+                                   n_global=n_global)
+        plan = plan_batch(0)
+        t_host = time.perf_counter()
+        setup["plan_host_ms"] = round((t_host - t_src) * 1e3, 1)
+        setup["plan_threads"] = fused.plan_threads()
         # fused lower bound: read the crop, read the background,
         # write the composite, once each
         mt, mb, ml, mr = fused.G.crop_margins(S, S, cfg.margins)
@@ -286,6 +300,8 @@ def main(argv=None):
                        for i, p in enumerate(plan.params)}
         else:
             runner = fused.PipeRunner(plan, dev)
+            setup["taps_device_ms"] = round((time.perf_counter() - t_host) * 1e3, 1)
+            setup["taps_host_tiles"] = runner.host_tiles
             if runner.split and not args.unsplit and not args.split:
                 # one launch: H pass, background copy, V pass + paste (ipp_pipe_fused)
                 algo = {"ipp_pipe_fused": plan.algo_bytes_hpass_bgcopy + plan.algo_bytes_vblend_bands}
@@ -361,6 +377,8 @@ def main(argv=None):
                 return res
         workload = "rotations+symmetry fused gather (NEAREST rotate, expand, bbox crop, flip)"
     plan_ms = (time.perf_counter() - t_plan) * 1e3
+    if "plan_host_ms" in setup:   # planning proper, without making the synthetic sources
+        plan_ms = setup["plan_host_ms"] + setup.get("taps_device_ms", 0.0)
 
     if args.dry_run:
         if world > 1:
@@ -405,6 +423,35 @@ def main(argv=None):
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    stream_res = None
+    if args.stream and args.workload == "pipe5":
+        # Streaming: batch k of the timed run has its own plan (seed + k),
+        # planned on a worker thread (host planner + device taps on a side
+        # stream) while batch k-1 runs.  The clock starts with the pipeline
+        # primed and stops when the last batch has finished.
+        ps = fused.PipeStream(dev, plan_batch)
+        clock = {}
+
+        def mark():
+            barrier(world, dev)
+            clock["t0"] = time.perf_counter()
+        mark.at = args.warmup
+        ps.run(args.warmup + args.steps, src, bgs, out, mark=mark, record=True)
+        barrier(world, dev)
+        s_elapsed = time.perf_counter() - clock["t0"]
+        if world > 1:
+            t = torch.tensor([s_elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            s_elapsed = float(t.item())
+        tim = ps.timing[args.warmup:]
+        kms = [a.elapsed_time(b) for a, b in ps.events[args.warmup:]]
+        stream_res = {"ms_per_step": round(s_elapsed / args.steps * 1e3, 3),
+                      "value": round(n_global * S * S / 1e6 * args.steps / s_elapsed, 1),
+                      "kernel_ms": round(float(np.mean(kms)), 4),
+                      "plan_host_ms": round(float(np.mean([t[0] for t in tim])), 2),
+                      "taps_device_ms": round(float(np.mean([t[1] for t in tim])), 2),
+                      "taps_host_tiles": round(float(np.mean([t[2] for t in tim])), 1)}
 
     if args.dump_digests:
         mine = outputs()
@@ -460,6 +507,11 @@ def main(argv=None):
         "kernels_algo_bytes": {k: int(v) for k, v in algo.items()},
         "plan_ms": round(plan_ms, 1),
     }
+    if setup:
+        result["setup_ms"] = setup
+    if stream_res is not None:
+        stream_res["vs_resident"] = round(stream_res["value"] / result["value"], 4)
+        result["stream"] = stream_res
     if fused_bound is not None:
         gbps = fused_bound / (ms_step * 1e-3) / 1e9
         result["fused_bound"] = {"bytes_per_item": fused_item, "bytes_per_step": int(fused_bound),

@@ -88,6 +88,29 @@ PASTE_DESC = np.dtype([
 PIPE_DESC = np.dtype([("g", GATHER_DESC), ("h", RESAMPLE_DESC), ("v", RESAMPLE_DESC), ("p", PASTE_DESC)],
                      align=True)
 
+PIPE_PLAN_CFG = np.dtype([
+    ("src_h", _I4), ("src_w", _I4), ("src_pitch", _I4), ("crop_t", _I4), ("crop_b", _I4), ("crop_l", _I4),
+    ("crop_r", _I4), ("bg_h", _I4), ("bg_w", _I4), ("n_bg", _I4), ("n_sym", _I4), ("sym_flip", _I4, (4,)),
+    ("n_global", _I4), ("start", _I4), ("stop", _I4), ("given", _I4), ("n_threads", _I4), ("seed", np.uint64),
+    ("angle_min", np.float64), ("angle_max", np.float64), ("scale_min", np.float64), ("scale_max", np.float64),
+], align=True)
+
+PIPE_ITEM = np.dtype([
+    ("angle", np.float64), ("ratio", np.float64), ("sym", _I4), ("bg_index", _I4), ("x", _I4), ("y", _I4),
+    ("rot_w", _I4), ("rot_h", _I4), ("cut_x", _I4), ("cut_y", _I4), ("cut_w", _I4), ("cut_h", _I4),
+    ("ov_w", _I4), ("ov_h", _I4),
+], align=True)
+
+TAP_AXIS = np.dtype([
+    ("in_size", _I4), ("out_size", _I4), ("identity", _I4), ("shift", _I4), ("phase", _I4), ("nkb", _I4),
+    ("tile0", _I4), ("n_tiles", _I4), ("coef_off", _I8),
+], align=True)
+
+# ipp_plan_pipe_batch totals[] slots (ipp.h IPP_PT_*)
+IPP_PLAN_TOTALS = 16
+PT = dict(coef_words=0, tmp_bytes=1, max_out_w=2, max_rows=3, max_ov_w=4, max_ov_h=5, algo_h=6, algo_v=7,
+          copy_bytes=8, max_tiles=9, err_item=10, err_code=11)
+
 # (symbol, restype, argtypes) — every entry point declared in include/ipp.h.
 _P = ctypes.c_void_p
 _I = ctypes.c_int32
@@ -128,6 +151,14 @@ SIGNATURES = {
     "ipp_enhance_color": (_I, [_P, _P, _P, _I, _L, _P, _P, _P]),
     "ipp_box_pass": (_I, [_P, _P, _P, _I, _L, _P, _I, _P, _I, _P]),
     "ipp_pipe_status": (_I, [_P, _P]),
+    "ipp_plan_pipe_batch": (_I, [_P, _P, _P, _P, _P]),
+    "ipp_pipe_taps_scratch_bytes": (_L, [_I]),
+    "ipp_pipe_plan_taps": (_I, [_P, _I, _P, _P, _P, _P]),
+    "ipp_plan_mfma_tile": (_I, [_P, _I, _P, _P, _P, _L]),
+    "ipp_plan_opaque_bbox_fast": (_I, [_I, _I, _P, _I, _I, _P]),
+    "ipp_plan_py_hypot": (_D, [_D, _D]),
+    "ipp_plan_rotation": (_I, [_I, _I, _D, _P]),
+    "ipp_plan_py_random": (_I, [ctypes.c_uint64, _I, _P]),
     "ipp_version": (ctypes.c_char_p, []),
 }
 

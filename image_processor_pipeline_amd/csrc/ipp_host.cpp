@@ -72,6 +72,34 @@ extern "C" int32_t ipp_plan_lanczos_ksize(double in0, double in1, int32_t out_si
     return ksize_of(in0, in1, out_size);
 }
 
+namespace {
+// One output of Resample.c precompute_coeffs + normalize_coeffs_8bpc: its
+// bounds and its `ksize` quantised taps (zero past the support).
+inline void lanczos_one(int32_t in_size, float fin0, double scale, double support, double ss, int xx, int ksize,
+                        double* k, int32_t* kq, int& xmin_out, int& cnt_out) {
+    const double center = fin0 + (xx + 0.5) * scale;
+    double ww = 0.0;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    for (int x = 0; x < xmax; ++x) {
+        const double w = lanczos_filter((x + xmin - center + 0.5) * ss);
+        k[x] = w;
+        ww += w;
+    }
+    for (int x = 0; x < xmax; ++x)
+        if (ww != 0.0) k[x] /= ww;
+    for (int x = 0; x < ksize; ++x) {
+        const double v = x < xmax ? k[x] : 0.0;
+        kq[x] = v < 0 ? (int32_t)(-0.5 + v * (1 << 22)) : (int32_t)(0.5 + v * (1 << 22));
+    }
+    xmin_out = xmin;
+    cnt_out = xmax;
+}
+}  // namespace
+
 extern "C" int64_t ipp_plan_lanczos(int32_t in_size, double in0, double in1, int32_t out_size, int32_t* out,
                                     int64_t out_capacity) {
     if (in_size <= 0 || out_size <= 0) return IPP_E_ARG;
@@ -88,27 +116,10 @@ extern "C" int64_t ipp_plan_lanczos(int32_t in_size, double in0, double in1, int
     std::vector<double> k(ksize);
     const double ss = 1.0 / filterscale;
     for (int xx = 0; xx < out_size; ++xx) {
-        const double center = fin0 + (xx + 0.5) * scale;
-        double ww = 0.0;
-        int xmin = (int)(center - support + 0.5);
-        if (xmin < 0) xmin = 0;
-        int xmax = (int)(center + support + 0.5);
-        if (xmax > in_size) xmax = in_size;
-        xmax -= xmin;
-        for (int x = 0; x < xmax; ++x) {
-            const double w = lanczos_filter((x + xmin - center + 0.5) * ss);
-            k[x] = w;
-            ww += w;
-        }
-        for (int x = 0; x < xmax; ++x)
-            if (ww != 0.0) k[x] /= ww;
-        int32_t* kq = kk + (int64_t)xx * ksize;
-        for (int x = 0; x < ksize; ++x) {
-            const double v = x < xmax ? k[x] : 0.0;
-            kq[x] = v < 0 ? (int32_t)(-0.5 + v * (1 << 22)) : (int32_t)(0.5 + v * (1 << 22));
-        }
+        int xmin, cnt;
+        lanczos_one(in_size, fin0, scale, support, ss, xx, ksize, k.data(), kk + (int64_t)xx * ksize, xmin, cnt);
         bounds[2 * xx] = xmin;
-        bounds[2 * xx + 1] = xmax;
+        bounds[2 * xx + 1] = cnt;
     }
     return ksize;
 }
@@ -331,6 +342,67 @@ extern "C" int ipp_plan_mfma_from_taps(int32_t in_size, int32_t out_size, int32_
             bias[16 * t + col] = (int32_t)((1 << 21) + 128 * sum);
         }
         boff += (int64_t)nK * 3 * 64;
+    }
+    return IPP_OK;
+}
+
+// One tile of an axis in the layout of the device tap planner (tile t's
+// blocks at uint4 offset t·nkb·192), from Pillow's taps computed here.
+extern "C" int ipp_plan_mfma_tile(const ipp_tap_axis* a, int32_t t, int32_t hdr[4], int32_t bias[16],
+                                  uint8_t* blocks, int64_t blocks_cap) {
+    if (!a || !hdr || !bias || !blocks || a->in_size <= 0 || a->out_size <= 0 || a->phase < 0 || a->phase > 15 ||
+        t < 0 || t >= (a->out_size + a->phase + 15) / 16)
+        return IPP_E_ARG;
+    const int in = a->in_size, out = a->out_size, shift = a->shift;
+    const int o0 = 16 * t - a->phase, o1 = std::min(o0 + 16, out), oa = std::max(o0, 0);
+    const float fin0 = 0.0f, fin1 = (float)in;
+    const double scale = (double)(fin1 - fin0) / out;
+    const double filterscale = scale < 1.0 ? 1.0 : scale;
+    const double support = 3.0 * filterscale, ss = 1.0 / filterscale;
+    const int ksize = a->identity ? 1 : (int)ceil(support) * 2 + 1;
+    std::vector<double> kd(ksize);
+    std::vector<int32_t> kq(16 * (size_t)ksize);
+    int xs[16], cn[16];
+    for (int o = oa; o < o1; ++o) {
+        const int c = o - o0;
+        if (a->identity) {
+            xs[c] = o;
+            cn[c] = 1;
+            kq[(size_t)c * ksize] = 1 << 22;
+        } else {
+            lanczos_one(in, fin0, scale, support, ss, o, ksize, kd.data(), kq.data() + (size_t)c * ksize, xs[c],
+                        cn[c]);
+        }
+        xs[c] -= shift;
+    }
+    if (xs[oa - o0] < 0) return IPP_E_RANGE;
+    const int K0 = xs[oa - o0] & ~15;
+    int end = K0;
+    for (int o = oa; o < o1; ++o) end = std::max(end, xs[o - o0] + cn[o - o0]);
+    const int nK = (end - K0 + 63) / 64;
+    if (nK > a->nkb || (int64_t)nK * 3072 > blocks_cap) return IPP_E_RANGE;
+    hdr[0] = K0;
+    hdr[1] = nK;
+    hdr[2] = t * a->nkb * 192;
+    hdr[3] = 0;
+    memset(blocks, 0, (size_t)nK * 3072);
+    for (int col = 0; col < 16; ++col) {
+        const int o = o0 + col;
+        if (o < oa || o >= o1) {
+            bias[col] = 0;
+            continue;
+        }
+        int64_t sum = 0;
+        for (int q = 0; q < cn[col]; ++q) {
+            const int32_t k = kq[(size_t)col * ksize + q];
+            sum += k;
+            int8_t b[3];
+            balanced_bytes(k, b);
+            const int rel = xs[col] + q - K0, s = rel / 64, kin = rel % 64;
+            const int lane = 16 * (kin / 16) + col, j = kin % 16;
+            for (int p = 0; p < 3; ++p) blocks[((int64_t)(s * 3 + p) * 64 + lane) * 16 + j] = (uint8_t)b[p];
+        }
+        bias[col] = (int32_t)((1 << 21) + 128 * sum);
     }
     return IPP_OK;
 }

@@ -18,7 +18,9 @@ device work is two launches for the whole batch (``ipp_pipe_hpass``,
 from __future__ import annotations
 
 import math
+import os
 import random
+import time
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
@@ -58,12 +60,12 @@ class ItemParams:
 
 @dataclass
 class PipePlan:
-    descs: np.ndarray            # PIPE_DESC[n]
-    coefs: np.ndarray            # int32 taps for all items
+    descs: np.ndarray            # PIPE_DESC[n], processing order (grouped by background)
+    axes: np.ndarray             # TAP_AXIS[2n]: H then V axis of each item (device tap planner)
+    coef_words: int              # int32 size of the device tap buffer
     hsv: np.ndarray              # HSV_PARAMS
-    params: List[ItemParams]
-    cut_dims: List[Tuple[int, int]]       # (h, w) of the cut-out M
-    ov_dims: List[Tuple[int, int]]        # (h, w) of the resized overlay
+    items: np.ndarray            # PIPE_ITEM[n]: drawn parameters and geometry, item order
+    sym_pool: Tuple[str, ...]    # items["sym"] indexes this pool
     tmp_bytes: int
     max_out_w: int
     max_rows: int
@@ -78,6 +80,22 @@ class PipePlan:
     # background rows outside the overlay bands move with the H pass
     algo_bytes_hpass_bgcopy: int = 0
     algo_bytes_vblend_bands: int = 0
+
+    @property
+    def params(self) -> List[ItemParams]:
+        it = self.items
+        return [ItemParams(float(a), self.sym_pool[s], int(b), float(r), int(x), int(y))
+                for a, s, b, r, x, y in zip(it["angle"], it["sym"], it["bg_index"], it["ratio"], it["x"], it["y"])]
+
+    @property
+    def cut_dims(self) -> List[Tuple[int, int]]:
+        """(h, w) of each item's cut-out M."""
+        return list(zip(self.items["cut_h"].tolist(), self.items["cut_w"].tolist()))
+
+    @property
+    def ov_dims(self) -> List[Tuple[int, int]]:
+        """(h, w) of each item's resized overlay."""
+        return list(zip(self.items["ov_h"].tolist(), self.items["ov_w"].tolist()))
 
 
 def draw_params(n_global: int, stop: int, src_hw: Tuple[int, int], bg_hw: Tuple[int, int], n_bg: int,
@@ -148,9 +166,33 @@ def shard_range(n_global: int, rank: int, world: int) -> Tuple[int, int]:
     return start, start + q + (1 if rank < rem else 0)
 
 
+def plan_threads() -> int:
+    """Host threads for the batch planner: the job's CPU share
+    (OMP_NUM_THREADS when set, else the CPUs this process may run on)."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    if n <= 0:
+        n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(n, 32))
+
+
+_PLAN_ERRORS = {
+    1: (NotImplementedError, "rotation canvas beyond Pillow's 16.16 fixed-point range (>32767 px)"),
+    2: (NotImplementedError, "non-affine ScaleAffine table"),
+    3: (ValueError, "degenerate overlay size"),
+    4: (ValueError, "parameters do not fit the background (position, background index or symmetry)"),
+    5: (ValueError, "LANCZOS downscale needs a tap window wider than the fused H pass's 512-column LDS ring; "
+                    "use the plugin path"),
+    6: (ValueError, "empty range for randrange() (overlay larger than the background)"),
+}
+
+
 def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int, cfg: PipeConfig,
               seed: int = 0, src_pitch: Optional[int] = None, item_range: Optional[Tuple[int, int]] = None,
-              n_global: Optional[int] = None, params: Optional[Sequence[ItemParams]] = None) -> PipePlan:
+              n_global: Optional[int] = None, params: Optional[Sequence[ItemParams]] = None,
+              n_threads: int = 0) -> PipePlan:
     """Plan `n` items.  The random stream is the one a chained file-mode
     ``ProcessingPipeline`` of the five reference steps over ``n_global``
     sources would consume under ``random.seed(seed)`` (``draw_params``).
@@ -160,147 +202,90 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     outputs do not depend on the number of GPUs.  ``n_global`` defaults to
     ``stop``.  With ``params`` (one ItemParams per item) nothing is drawn:
     the caller's angles, symmetries, backgrounds, ratios and positions are
-    planned as given (positions must keep the overlay inside the background)."""
+    planned as given (positions must keep the overlay inside the background).
+
+    The whole plan is one call of the threaded C planner
+    (``ipp_plan_pipe_batch``: CPython's MT19937 draws, Pillow's rotate
+    geometry, the opaque getbbox, the overlay size, the descriptors); the
+    LANCZOS taps are built later on the device (``PipeRunner``)."""
     H, W = src_hw
     bh, bw = bg_hw
     start, stop = item_range if item_range is not None else (0, n)
-    if stop - start != n or start < 0:
+    if stop - start != n or start < 0 or n <= 0:
         raise ValueError(f"item_range {item_range} does not hold {n} items")
     n_global = stop if n_global is None else n_global
     if n_global < stop:
         raise ValueError(f"n_global {n_global} < item_range stop {stop}")
     t, b, l, r = G.crop_margins(H, W, cfg.margins)
-    wc, hc = W - l - r, H - t - b
-    if params is None:
+    items = np.zeros(n, N.PIPE_ITEM)
+    c = np.zeros((), N.PIPE_PLAN_CFG)
+    pool = tuple(cfg.sym_pool)
+    given = params
+    if given is None and not (isinstance(seed, int) and abs(seed) < 1 << 64):
+        # seeds the C generator does not take (floats, strings, > 64 bits):
+        # draw in Python, plan the draws as given parameters
         angles, syms, order, drawn = draw_params(n_global, stop, src_hw, bg_hw, n_bg, cfg, seed)
-        given = None
+        given = [ItemParams(angles[g], syms[g], order[g % n_bg], drawn[g][0], drawn[g][1], drawn[g][2])
+                 for g in range(start, stop)]
+    if given is not None:
+        if len(given) != n:
+            raise ValueError(f"{len(given)} ItemParams for {n} items")
+        pool = ALL_SYMS
+        for i, it in enumerate(given):
+            if it.sym not in SYM_FLIP:
+                raise ValueError(f"item {start + i}: parameters {it} do not fit a {bw}x{bh} background")
+        items["angle"] = [it.angle for it in given]
+        items["ratio"] = [it.ratio for it in given]
+        items["sym"] = [ALL_SYMS.index(it.sym) for it in given]
+        items["bg_index"] = [it.bg_index for it in given]
+        items["x"] = [it.x for it in given]
+        items["y"] = [it.y for it in given]
+        c["given"] = 1
     else:
-        if len(params) != n:
-            raise ValueError(f"{len(params)} ItemParams for {n} items")
-        given = list(params)
-    d = np.zeros(n, N.PIPE_DESC)
-    params: List[ItemParams] = []
-    cut_dims, ov_dims = [], []
-    # axis list for the batch tap planner: (in, out) pairs, H then V per item
-    axes_in, axes_out, identity = [], [], []
-    for gi in range(start, stop):
-        i = gi - start
-        if given is None:
-            ratio, x, y, plan, (ox, oy, rw, rh), (nw_, nh_) = drawn[gi]
-            angle, sym, bgi = angles[gi], syms[gi], order[gi % n_bg]
-        else:
-            it = given[i]
-            angle, sym, bgi, ratio, x, y = it.angle, it.sym, it.bg_index, it.ratio, it.x, it.y
-            plan, (ox, oy, rw, rh), (nw_, nh_) = item_geometry(wc, hc, angle, ratio, bw, bh, gi)
-            if not (0 <= x <= bw - nw_ and 0 <= y <= bh - nh_ and 0 <= bgi < n_bg and sym in SYM_FLIP):
-                raise ValueError(f"item {gi}: parameters {it} do not fit a {bw}x{bh} background")
-        params.append(ItemParams(angle, sym, bgi, ratio, x, y))
-        cut_dims.append((rh, rw))
-        ov_dims.append((nh_, nw_))
-        g = d[i]["g"]
-        g["src_off"] = i * H * (src_pitch or 3 * W)
-        g["src_pitch"] = src_pitch or 3 * W
-        g["src_cn"] = 3
-        g["src_w"], g["src_h"] = W, H
-        g["in_x0"], g["in_y0"], g["in_w"], g["in_h"] = l, t, wc, hc
-        for k in range(6):
-            g[f"a{k}"] = plan.A[k]
-        g["out_w"], g["out_h"] = rw, rh
-        g["off_x"], g["off_y"] = ox, oy
-        g["flip"] = SYM_FLIP[sym]
-        same = (nw_, nh_) == (rw, rh)
-        identity.append((same or nw_ == rw, same or nh_ == rh))
-        axes_in += [rw, rh]
-        axes_out += [nw_, nh_]
-
-    # ---- taps (C planner, threaded; MFMA tile format, see ipp_host.cpp) -----
+        if not 1 <= len(pool) <= 4 or any(p not in SYM_FLIP for p in pool):
+            raise ValueError(f"symmetry pool {pool}: 1 to 4 of {ALL_SYMS}")
+        c["seed"] = abs(seed)
+    c["src_h"], c["src_w"], c["src_pitch"] = H, W, src_pitch or 0
+    c["crop_t"], c["crop_b"], c["crop_l"], c["crop_r"] = t, b, l, r
+    c["bg_h"], c["bg_w"], c["n_bg"] = bh, bw, n_bg
+    c["n_sym"] = len(pool)
+    c["sym_flip"][:len(pool)] = [SYM_FLIP[p] for p in pool]
+    c["n_global"], c["start"], c["stop"] = n_global, start, stop
+    c["angle_min"], c["angle_max"] = cfg.angle_min, cfg.angle_max
+    c["scale_min"], c["scale_max"] = cfg.scale_min, cfg.scale_max
+    c["n_threads"] = n_threads or plan_threads()
+    descs = np.zeros(n, N.PIPE_DESC)
+    axes = np.zeros(2 * n, N.TAP_AXIS)
+    tot = np.zeros(N.IPP_PLAN_TOTALS, np.int64)
     lib = N.load()
-    m = 2 * n
-    a_in = np.asarray(axes_in, np.int32)
-    a_out = np.asarray(axes_out, np.int32)
-    ident = np.array([identity[j // 2][j % 2] for j in range(m)], np.int32)
-    # V axes are shifted to ybox_first whenever Pillow runs the H pass
-    shift = np.array([(j % 2 == 1) and not identity[j // 2][0] for j in range(m)], np.int32)
-    ks = np.array([1 if ident[j] else lib.ipp_plan_lanczos_ksize(0.0, float(a_in[j]), int(a_out[j]))
-                   for j in range(m)], np.int64)
-    # The H pass keeps each output tile's input window in a 512-column LDS ring
-    # (ipp_pipe.hip RING): 64·nK columns must fit.
-    for j in range(0, m, 2):
-        if ident[j]:
-            continue
-        cols = 64 * lib.ipp_plan_mfma_nk_bound(int(a_in[j]), int(a_out[j]), int(ks[j]))
-        if cols > H_RING_COLUMNS:
-            raise ValueError(f"item {j // 2}: LANCZOS downscale {a_in[j]} -> {a_out[j]} needs a {cols}-column "
-                             f"window, more than the fused H pass holds ({H_RING_COLUMNS}); use the plugin path")
-    # H axes (even j): tiles of 16 outputs; V axes: tiles aligned with 16-row
-    # background bands (phase = y mod 16)
-    transp = np.array([2 if j % 2 == 0 else 2 + params[j // 2].y % 16 for j in range(m)], np.int32)
-    sizes = np.array([lib.ipp_plan_mfma_size(int(a_in[j]), int(a_out[j]), int(ks[j])) for j in range(m)],
-                     np.int64)
-    sizes = (sizes + 3) // 4 * 4          # 16-B aligned axis blocks
-    offs = np.zeros(m, np.int64)
-    offs[1:] = np.cumsum(sizes)[:-1]
-    coefs = np.zeros(int(sizes.sum()), np.int32)
-    first_last = np.zeros(2 * m, np.int32)
-    N.check(lib.ipp_plan_pipe_axes(m, N.np_ptr(a_in), N.np_ptr(a_out), N.np_ptr(ident), N.np_ptr(shift),
-                                   N.np_ptr(transp), N.np_ptr(offs), N.np_ptr(coefs), N.np_ptr(first_last), 0),
-            "ipp_plan_pipe_axes")
-
-    # ---- descriptors ----------------------------------------------------
-    tmp_off = 0
-    max_out_w = max_rows = 1
-    algo_h = algo_v = copy_rows = 0
-    for i in range(n):
-        rh, rw = cut_dims[i]
-        nh_, nw_ = ov_dims[i]
-        jh, jv = 2 * i, 2 * i + 1
-        if not identity[i][0]:
-            y0, y1 = int(first_last[2 * jv]), int(first_last[2 * jv + 1])
-        else:
-            y0, y1 = 0, rh
-        rows = y1 - y0
-        # V tiles read up to 64·nK rows past their 16-aligned start
-        nkb = lib.ipp_plan_mfma_nk_bound(int(a_in[jv]), int(a_out[jv]), int(ks[jv]))
-        groups = (((rows + 15) // 16) * 16 + 64 * nkb + 16) // 4
-        pitch = 16 * nw_
-        h = d[i]["h"]
-        h["dst_off"] = tmp_off
-        h["dst_pitch"] = pitch
-        h["in_len"], h["out_len"], h["lines"], h["line0"], h["ksize"] = rw, nw_, rows, y0, ks[jh]
-        h["coef_off"] = offs[jh]
-        v = d[i]["v"]
-        v["src_off"] = tmp_off
-        v["src_pitch"] = pitch
-        v["in_len"], v["out_len"], v["lines"], v["ksize"] = rows, nh_, nw_, ks[jv]
-        v["coef_off"] = offs[jv]
-        p = d[i]["p"]
-        it = params[i]
-        p["bg_off"] = it.bg_index * bh * bw * 3
-        p["dst_off"] = i * bh * bw * 3
-        p["bg_w"], p["bg_h"], p["bg_pitch"], p["dst_pitch"] = bw, bh, 3 * bw, 3 * bw
-        p["ov_w"], p["ov_h"], p["ov_pitch"], p["x"], p["y"] = nw_, nh_, 4 * nw_, it.x, it.y
-        tmp_off += pitch * groups
-        tmp_off = (tmp_off + 255) // 256 * 256
-        max_out_w = max(max_out_w, nw_)
-        max_rows = max(max_rows, rows)
-        t_bytes = pitch * ((rows + 3) // 4)
-        algo_h += 3 * hc * wc + t_bytes
-        algo_v += t_bytes + 3 * bh * bw + 3 * bh * bw
-        vb0 = (it.y // 16) * 16                      # overlay bands (ipp.h, ipp_pipe_vblend_bands)
-        vb1 = max(vb0, min(bh, -(-(it.y + nh_) // 16) * 16))
-        copy_rows += bh - (vb1 - vb0)
-    # Processing order: group items by background so that the items pasting
-    # onto one background run back to back (and, through the XCD-aware block
-    # mapping, on one XCD): the 3 MB background then stays in L2/L3 instead of
-    # being re-read from HBM per item.  Outputs keep their item offsets.
-    order = np.argsort(np.array([it.bg_index for it in params]), kind="stable")
-    d = d[order]
+    rc = lib.ipp_plan_pipe_batch(N.np_ptr(c), N.np_ptr(items), N.np_ptr(descs), N.np_ptr(axes), N.np_ptr(tot))
+    if rc == N.IPP_E_RANGE and int(tot[N.PT["err_code"]]) in _PLAN_ERRORS:
+        exc, msg = _PLAN_ERRORS[int(tot[N.PT["err_code"]])]
+        raise exc(f"item {int(tot[N.PT['err_item']])}: {msg}")
+    N.check(rc, "ipp_plan_pipe_batch")
+    T = {k: int(tot[v]) for k, v in N.PT.items()}
     hsv = G.hsv_params(cfg.hsv_ranges, cfg.zones, cfg.use_gimp_scale, bgr=False)
-    copy_bytes = 2 * 3 * bw * copy_rows           # read + write of the rows outside the bands
-    return PipePlan(d, coefs, hsv, params, cut_dims, ov_dims, max(tmp_off, 256), max_out_w, max_rows, bw, bh,
-                    algo_h, algo_v, N.IPP_TAPS_MFMA,
-                    max(w for _, w in ov_dims), max(h for h, _ in ov_dims),
-                    algo_h + copy_bytes, algo_v - copy_bytes)
+    return PipePlan(descs, axes, T["coef_words"], hsv, items, pool, T["tmp_bytes"], T["max_out_w"], T["max_rows"],
+                    bw, bh, T["algo_h"], T["algo_v"], N.IPP_TAPS_MFMA, T["max_ov_w"], T["max_ov_h"],
+                    T["algo_h"] + T["copy_bytes"], T["algo_v"] - T["copy_bytes"])
+
+
+def plan_taps(plan: PipePlan, device, stream=None) -> Tuple[torch.Tensor, int]:
+    """The plan's LANCZOS taps, built on the device (ipp_pipe_plan_taps):
+    returns (int32 tensor of plan.coef_words (+ slack), tiles rebuilt on the
+    host).  Synchronises the stream."""
+    lib = N.load()
+    device = torch.device(device)
+    coefs = torch.empty(plan.coef_words + 4096, dtype=torch.int32, device=device)
+    nb = lib.ipp_pipe_taps_scratch_bytes(len(plan.axes))
+    scratch = torch.empty(int(nb), dtype=torch.uint8, device=device)
+    stats = np.zeros(2, np.int64)
+    N.check(lib.ipp_pipe_plan_taps(N.np_ptr(plan.axes), len(plan.axes), coefs.data_ptr(), scratch.data_ptr(),
+                                   N.np_ptr(stats), stream if stream is not None else _stream(device)),
+            "ipp_pipe_plan_taps")
+    if stats[1]:
+        raise N.NativeError(f"ipp_pipe_plan_taps: device status {int(stats[1])} (tile beyond its K-step bound)")
+    return coefs, int(stats[0])
 
 
 class PipeRunner:
@@ -310,7 +295,7 @@ class PipeRunner:
         self.plan = plan
         self.device = torch.device(device)
         self.descs = _to_dev(plan.descs, self.device)
-        self.coefs = torch.from_numpy(plan.coefs).to(self.device)
+        self.coefs, self.host_tiles = plan_taps(plan, self.device)
         self.tmp = torch.empty(plan.tmp_bytes, dtype=torch.uint8, device=self.device)
         self.lib = N.load()
         nb = self.lib.ipp_pipe_sync_bytes(len(plan.descs), plan.bg_h, plan.max_ov_h)
@@ -383,3 +368,87 @@ class PipeRunner:
             self.hpass(src)
             self.vblend(bgs, out)
         return out
+
+
+class PipeStream:
+    """Streaming form of PipeRunner (bench.py --stream): every batch has its
+    own plan, built while the previous batch runs.  A worker thread runs
+    batch k+1's host plan (ipp_plan_pipe_batch; ctypes drops the GIL) and
+    its device taps (ipp_pipe_plan_taps on a side stream) while batch k's
+    fused launch runs on the caller's stream.  Device buffers live in
+    `slots` sets that alternate; a set is refilled only after the batch that
+    last used it has completed (its HIP event)."""
+
+    def __init__(self, device, plan_fn, slots: int = 2):
+        self.device = torch.device(device)
+        self.plan_fn = plan_fn                  # batch index -> PipePlan
+        self.lib = N.load()
+        self.side = torch.cuda.Stream(self.device)
+        self.slots = [{"done": torch.cuda.Event(), "bufs": {}} for _ in range(max(2, slots))]
+        self.timing: List[Tuple[float, float, int]] = []   # per batch: host plan ms, taps ms, host tiles
+        self.events: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []
+
+    def _buf(self, slot, name: str, nbytes: int) -> torch.Tensor:
+        b = slot["bufs"].get(name)
+        if b is None or b.numel() < nbytes:
+            slot["bufs"][name] = None
+            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+            slot["bufs"][name] = b
+        return b
+
+    def _prepare(self, k: int, slot):
+        t0 = time.perf_counter()
+        plan = self.plan_fn(k)
+        t1 = time.perf_counter()
+        slot["done"].synchronize()              # the batch that used these buffers has finished
+        n = len(plan.descs)
+        nsync = self.lib.ipp_pipe_sync_bytes(n, plan.bg_h, plan.max_ov_h)
+        if nsync < 0:
+            raise N.NativeError(f"ipp_pipe_sync_bytes({n}, {plan.bg_h}, {plan.max_ov_h}) failed")
+        bufs = {"descs": self._buf(slot, "descs", plan.descs.nbytes),
+                "coefs": self._buf(slot, "coefs", 4 * (plan.coef_words + 4096)),
+                "tmp": self._buf(slot, "tmp", plan.tmp_bytes),
+                "sync": self._buf(slot, "sync", nsync),
+                "scratch": self._buf(slot, "scratch", self.lib.ipp_pipe_taps_scratch_bytes(len(plan.axes)))}
+        stats = np.zeros(2, np.int64)
+        with torch.cuda.stream(self.side):
+            bufs["descs"][:plan.descs.nbytes].copy_(torch.from_numpy(plan.descs.view(np.uint8)))
+            N.check(self.lib.ipp_pipe_plan_taps(N.np_ptr(plan.axes), len(plan.axes), bufs["coefs"].data_ptr(),
+                                                bufs["scratch"].data_ptr(), N.np_ptr(stats),
+                                                self.side.cuda_stream), "ipp_pipe_plan_taps")
+        if stats[1]:
+            raise N.NativeError(f"ipp_pipe_plan_taps: device status {int(stats[1])}")
+        t2 = time.perf_counter()
+        return plan, bufs, ((t1 - t0) * 1e3, (t2 - t1) * 1e3, int(stats[0]))
+
+    def run(self, n_batches: int, src: torch.Tensor, bgs: torch.Tensor, out: torch.Tensor, mark=None,
+            record: bool = False) -> None:
+        """Run batches 0 .. n_batches-1 (plan_fn(k) plans batch k).  `mark`
+        (optional callable) is called right before batch `mark.at` is
+        launched, with the pipeline primed (its plan ready, the next one not
+        yet started) — bench.py starts its clock there."""
+        from concurrent.futures import ThreadPoolExecutor
+        main = torch.cuda.current_stream(self.device)
+        with ThreadPoolExecutor(1) as ex:
+            fut = ex.submit(self._prepare, 0, self.slots[0])
+            for k in range(n_batches):
+                plan, b, tm = fut.result()
+                if mark is not None and k == mark.at:
+                    mark()
+                slot = self.slots[k % len(self.slots)]
+                if k + 1 < n_batches:
+                    fut = ex.submit(self._prepare, k + 1, self.slots[(k + 1) % len(self.slots)])
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if record else None
+                if ev:
+                    ev[0].record(main)
+                N.check(self.lib.ipp_pipe_fused(src.data_ptr(), b["tmp"].data_ptr(), b["coefs"].data_ptr(),
+                                                b["descs"].data_ptr(), len(plan.descs), plan.max_out_w,
+                                                plan.max_rows, 3, N.np_ptr(plan.hsv), plan.tap_format,
+                                                bgs.data_ptr(), out.data_ptr(), plan.bg_w, plan.bg_h,
+                                                plan.max_ov_w, plan.max_ov_h, b["sync"].data_ptr(),
+                                                main.cuda_stream), "ipp_pipe_fused")
+                if ev:
+                    ev[1].record(main)
+                    self.events.append(ev)
+                slot["done"].record(main)
+                self.timing.append(tm)

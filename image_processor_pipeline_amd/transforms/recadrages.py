@@ -120,6 +120,12 @@ def fit_crop(image_path: Path, output_dirs: List[Path], **options: Any) -> Optio
     # pixel are a non-zero pixel.
     if image.mode in ("RGBA", "LA", "PA", "RGBa", "La"):
         bb = D.alpha_bbox([t])[0]
+    elif bpp == 2:
+        # 2-byte modes (I;16, I;16B, …) are stored through Pillow's image8
+        # rows, so GetBBox.c scans only the first `w` BYTES of each row and
+        # reports byte columns as pixel x coordinates
+        head = _rt.h2d(np.ascontiguousarray(px.reshape(h, 2 * w)[:, :w]).reshape(h, w, 1))
+        bb = D.alpha_bbox([head])[0]
     else:
         bb = D.alpha_bbox([t.view(h, w * bpp, 1)])[0]
         if bb:

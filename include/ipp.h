@@ -374,6 +374,98 @@ int ipp_plan_opaque_bbox(int32_t in_w, int32_t in_h, const int32_t a[6],
                          int32_t nw, int32_t nh, int32_t bbox[4]);
 
 /* ------------------------------------------------------------------------ */
+/* Batch planner of the fused pipe (ipp_plan.cpp; replaces the per-item host  */
+/* loop of fused.plan_pipe).  Draws every random parameter in the order of    */
+/* the reference's chained file-mode pipeline with CPython's generator        */
+/* (rotations.py:89, symmetry.py:122, pipeline.py:202, overlays.py:108,       */
+/* :133-134), plans each item's geometry (rotations.py:96-109,                */
+/* overlays.py:106-126) and fills the pipe descriptors (grouped by background) */
+/* and the per-axis records of the device tap planner.                        */
+/* ------------------------------------------------------------------------ */
+typedef struct ipp_pipe_plan_cfg {
+    int32_t src_h, src_w, src_pitch;          /* RGB u8 sources; pitch 0 = 3·src_w */
+    int32_t crop_t, crop_b, crop_l, crop_r;   /* crop_from_border margins (px)     */
+    int32_t bg_h, bg_w, n_bg;
+    int32_t n_sym, sym_flip[4];               /* symmetry pool (flip code per entry) */
+    int32_t n_global, start, stop;            /* plan items [start, stop) of n_global */
+    int32_t given;                            /* 1: items[] hold angle, ratio, sym,
+                                                 bg_index, x, y (nothing is drawn) */
+    int32_t n_threads;                        /* ≤ 0: all cores                    */
+    uint64_t seed;                            /* |n| of random.seed(n)             */
+    double angle_min, angle_max, scale_min, scale_max;
+} ipp_pipe_plan_cfg;
+
+typedef struct ipp_pipe_item {
+    double angle, ratio;
+    int32_t sym, bg_index, x, y;              /* sym: index into the pool          */
+    int32_t rot_w, rot_h;                     /* rotated canvas (expand=True)      */
+    int32_t cut_x, cut_y, cut_w, cut_h;       /* its getbbox = the cut-out         */
+    int32_t ov_w, ov_h;                       /* resized overlay                   */
+} ipp_pipe_item;
+
+/* One resampling axis (2 per item: H then V) for ipp_pipe_plan_taps. */
+typedef struct ipp_tap_axis {
+    int32_t in_size, out_size;
+    int32_t identity;     /* 1: no pass on this axis (single 2^22 tap)        */
+    int32_t shift;        /* subtracted from every xmin (V axis: ybox_first)  */
+    int32_t phase;        /* tile phase (V axis: y mod 16)                    */
+    int32_t nkb;          /* ipp_plan_mfma_nk_bound: K-step slots per tile     */
+    int32_t tile0;        /* unused (0)                                       */
+    int32_t n_tiles;      /* (out_size + phase + 15) / 16                     */
+    int64_t coef_off;     /* int32 index of the axis block in coefs           */
+} ipp_tap_axis;
+
+/* totals[] slots of ipp_plan_pipe_batch */
+#define IPP_PT_COEF_WORDS 0   /* int32 size of the coefs buffer               */
+#define IPP_PT_TMP_BYTES 1
+#define IPP_PT_MAX_OUT_W 2
+#define IPP_PT_MAX_ROWS 3
+#define IPP_PT_MAX_OV_W 4
+#define IPP_PT_MAX_OV_H 5
+#define IPP_PT_ALGO_H 6       /* algorithmic bytes, see fused.PipePlan        */
+#define IPP_PT_ALGO_V 7
+#define IPP_PT_COPY_BYTES 8
+#define IPP_PT_MAX_TILES 9
+#define IPP_PT_ERR_ITEM 10    /* on IPP_E_RANGE: global item index and reason: */
+#define IPP_PT_ERR_CODE 11    /* 1 canvas beyond 16.16, 2 ScaleAffine table,
+                                 3 degenerate overlay, 4 given parameters do not
+                                 fit, 5 H window beyond the LDS ring, 6 empty
+                                 randint range                                 */
+#define IPP_PLAN_TOTALS 16
+
+/* items[stop - start]: outputs (inputs too when cfg->given); descs[n] (in
+ * processing order), axes[2n]; totals[IPP_PLAN_TOTALS]. */
+int ipp_plan_pipe_batch(const ipp_pipe_plan_cfg* cfg, ipp_pipe_item* items, ipp_pipe_desc* descs,
+                        ipp_tap_axis* axes, int64_t* totals);
+
+/* Device tap planner (ipp_taps.hip): builds the MFMA tile format of every
+ * axis (what ipp_plan_mfma_from_taps writes from Pillow's taps: hdr, bias,
+ * blocks; tile t's blocks at uint4 offset t·nkb·192 of the axis's block area)
+ * directly in `coefs` (device, IPP_PT_COEF_WORDS int32).  The taps are
+ * computed in fp64 on the device; any tile holding a tap whose rounding point
+ * lies within 2^-22 of a quantisation boundary is recomputed on the host with
+ * the libm sin Pillow uses and copied over, so the result is bit-exact with
+ * Resample.c.  scratch: device, ipp_pipe_taps_scratch_bytes(n_axes).
+ * Synchronises `stream`.  stats[0] = tiles recomputed on the host, stats[1] =
+ * device status (bit 0: a tile needed more K steps than nkb). */
+int64_t ipp_pipe_taps_scratch_bytes(int32_t n_axes);
+int ipp_pipe_plan_taps(const ipp_tap_axis* axes, int32_t n_axes, int32_t* coefs, void* scratch,
+                       int64_t* stats, void* stream);
+/* Host restatement of one tile of that format (Resample.c taps, libm sin):
+ * hdr[4], bias[16], blocks (nK·3072 bytes, ≤ blocks_cap). */
+int ipp_plan_mfma_tile(const ipp_tap_axis* axis, int32_t t, int32_t hdr[4], int32_t bias[16],
+                       uint8_t* blocks, int64_t blocks_cap);
+/* Pieces of ipp_plan_pipe_batch exposed for the tests: the division-free
+ * form of ipp_plan_opaque_bbox, CPython's math.hypot (vector_norm), the
+ * rotation plan (out = nw, nh, a0..a5) and the first n random() values of
+ * random.seed(seed). */
+int ipp_plan_opaque_bbox_fast(int32_t in_w, int32_t in_h, const int32_t a[6],
+                              int32_t nw, int32_t nh, int32_t bbox[4]);
+double ipp_plan_py_hypot(double x, double y);
+int ipp_plan_rotation(int32_t w, int32_t h, double angle, int32_t out[8]);
+int ipp_plan_py_random(uint64_t seed, int32_t n, double* out);
+
+/* ------------------------------------------------------------------------ */
 /* tranfo.enhance_image (transforms/tranfo.py:37-53) on RGB images:           */
 /* ImageEnhance Brightness/Contrast/Color (:38-40, Image.blend, Blend.c),     */
 /* GaussianBlur (:42-44, BoxBlur.c) and the r/g/b point() LUTs (:46-51).      */

@@ -42,6 +42,9 @@ STRUCTS = {
     "ipp_ccl_work": N.CCL_WORK,
     "ipp_affine_desc": N.AFFINE_DESC,
     "ipp_enhance_desc": N.ENHANCE_DESC,
+    "ipp_pipe_plan_cfg": N.PIPE_PLAN_CFG,
+    "ipp_pipe_item": N.PIPE_ITEM,
+    "ipp_tap_axis": N.TAP_AXIS,
 }
 
 

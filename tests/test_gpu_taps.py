@@ -1,0 +1,73 @@
+"""Device tap planner (ipp_taps.hip, ipp_pipe_plan_taps) against the host
+restatement of Pillow's taps (ipp_plan_mfma_tile: Resample.c
+precompute_coeffs + normalize_coeffs_8bpc with libm sin, reference call site
+overlays.py:129), tile by tile: header, biases and every byte of the i8
+blocks, bit-exact.  The host builder itself is pinned to the axis planner
+(tests/test_plan_batch.py) and that to the oracle (tests/test_host_plan.py).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from image_processor_pipeline_amd import _native as N
+from image_processor_pipeline_amd import fused as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _check_axes(plan, coefs, axes_idx):
+    lib = N.load()
+    c = coefs.cpu().numpy()
+    bad = []
+    for j in axes_idx:
+        a = plan.axes[j:j + 1]
+        T, off, nkb = int(a["n_tiles"][0]), int(a["coef_off"][0]), int(a["nkb"][0])
+        hdr = c[off:off + 4 * T].reshape(T, 4)
+        bias = c[off + 4 * T:off + 20 * T]
+        blocks = c[off + 20 * T:].view(np.uint8)
+        for t in range(T):
+            h4, b16 = np.zeros(4, np.int32), np.zeros(16, np.int32)
+            blk = np.zeros(nkb * 3072, np.uint8)
+            assert lib.ipp_plan_mfma_tile(N.np_ptr(a), t, N.np_ptr(h4), N.np_ptr(b16), N.np_ptr(blk), blk.size) == 0
+            nk = int(h4[1])
+            ok = (np.array_equal(hdr[t], h4) and np.array_equal(bias[16 * t:16 * t + 16], b16)
+                  and np.array_equal(blocks[h4[2] * 16:h4[2] * 16 + nk * 3072], blk[:nk * 3072]))
+            if not ok:
+                bad.append((j, t))
+    return bad
+
+
+@pytest.mark.parametrize("case", [
+    ((1024, 1024), 300, (1024, 1024), 16, F.PipeConfig(), 0),
+    ((96, 80), 40, (64, 72), 5, F.PipeConfig(margins=(8, 8, 8, 8)), 1246),
+    ((480, 640), 25, (720, 1280), 7, F.PipeConfig(margins=(0, 0, 0, 0), scale_min=0.4, scale_max=0.9), 3),
+    # upscales (ratio > source) and near-identity axes
+    ((200, 160), 30, (1024, 1024), 2, F.PipeConfig(margins=(0, 0, 0, 0), scale_min=0.5, scale_max=0.9), 11),
+])
+def test_device_taps_equal_host_taps(case):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    src_hw, n, bg_hw, n_bg, cfg, seed = case
+    plan = F.plan_pipe(src_hw, n, bg_hw, n_bg, cfg, seed=seed)
+    coefs, fixed = F.plan_taps(plan, DEV)
+    torch.cuda.synchronize()
+    bad = _check_axes(plan, coefs, range(len(plan.axes)))
+    print(f"host-rebuilt tiles: {fixed}")
+    assert not bad, bad[:10]
+
+
+def test_device_taps_bench_plan():
+    """The bench's B = 4096 plan: a seeded sample of 600 axes (every tile of
+    each), plus the count of host-rebuilt tiles stays small."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    plan = F.plan_pipe((1024, 1024), 4096, (1024, 1024), 16, F.PipeConfig(), seed=0)
+    coefs, fixed = F.plan_taps(plan, DEV)
+    torch.cuda.synchronize()
+    idx = np.random.default_rng(0).choice(len(plan.axes), 600, replace=False)
+    bad = _check_axes(plan, coefs, sorted(idx.tolist()) + [0, 1, len(plan.axes) - 2, len(plan.axes) - 1])
+    print(f"host-rebuilt tiles: {fixed}")
+    assert not bad, bad[:10]
+    assert fixed < 2000
