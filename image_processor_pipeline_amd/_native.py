@@ -91,7 +91,8 @@ PIPE_DESC = np.dtype([("g", GATHER_DESC), ("h", RESAMPLE_DESC), ("v", RESAMPLE_D
 PIPE_PLAN_CFG = np.dtype([
     ("src_h", _I4), ("src_w", _I4), ("src_pitch", _I4), ("crop_t", _I4), ("crop_b", _I4), ("crop_l", _I4),
     ("crop_r", _I4), ("bg_h", _I4), ("bg_w", _I4), ("n_bg", _I4), ("n_sym", _I4), ("sym_flip", _I4, (4,)),
-    ("n_global", _I4), ("start", _I4), ("stop", _I4), ("given", _I4), ("n_threads", _I4), ("seed", np.uint64),
+    ("n_global", _I4), ("start", _I4), ("stop", _I4), ("given", _I4), ("n_threads", _I4),
+    ("ring_cols", _I4), ("pad_", _I4), ("seed", np.uint64),
     ("angle_min", np.float64), ("angle_max", np.float64), ("scale_min", np.float64), ("scale_max", np.float64),
 ], align=True)
 

@@ -427,6 +427,7 @@ extern "C" int ipp_plan_pipe_batch(const ipp_pipe_plan_cfg* cfg, ipp_pipe_item* 
     const int32_t bw = c.bg_w, bh = c.bg_h;
     int nt = c.n_threads > 0 ? c.n_threads : (int)std::thread::hardware_concurrency();
     nt = std::max(1, std::min(nt, 64));
+    const int64_t ring = c.ring_cols > 0 ? c.ring_cols : 512;  // ipp_pipe.hip RING
 
     auto fail = [&](int64_t item, int code) {
         totals[IPP_PT_ERR_ITEM] = item;
@@ -560,7 +561,7 @@ extern "C" int ipp_plan_pipe_batch(const ipp_pipe_plan_cfg* cfg, ipp_pipe_item* 
         const int32_t rows = y1 - y0;
         const int32_t nkb_h = ipp_plan_mfma_nk_bound(rw, nw_, ks_h);
         const int32_t nkb_v = ipp_plan_mfma_nk_bound(rh, nh_, ks_v);
-        if (!id_h && 64 * nkb_h > 512) return fail(start + i, E_RING);
+        if (!id_h && 64 * (int64_t)nkb_h > ring) return fail(start + i, E_RING);
         ah = {rw, nw_, id_h ? 1 : 0, 0, 0, nkb_h, 0, (nw_ + 15) / 16, coef_words};
         coef_words += (ipp_plan_mfma_size(rw, nw_, ks_h) + 3) / 4 * 4;
         const int32_t phase = it.y % 16;

@@ -254,6 +254,7 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     c["angle_min"], c["angle_max"] = cfg.angle_min, cfg.angle_max
     c["scale_min"], c["scale_max"] = cfg.scale_min, cfg.scale_max
     c["n_threads"] = n_threads or plan_threads()
+    c["ring_cols"] = H_RING_COLUMNS
     descs = np.zeros(n, N.PIPE_DESC)
     axes = np.zeros(2 * n, N.TAP_AXIS)
     tot = np.zeros(N.IPP_PLAN_TOTALS, np.int64)

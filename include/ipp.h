@@ -391,6 +391,9 @@ typedef struct ipp_pipe_plan_cfg {
     int32_t given;                            /* 1: items[] hold angle, ratio, sym,
                                                  bg_index, x, y (nothing is drawn) */
     int32_t n_threads;                        /* ≤ 0: all cores                    */
+    int32_t ring_cols;                        /* H-pass LDS ring (≤ 0: 512); an H tile
+                                                 needing a wider window is refused */
+    int32_t pad_;
     uint64_t seed;                            /* |n| of random.seed(n)             */
     double angle_min, angle_max, scale_min, scale_max;
 } ipp_pipe_plan_cfg;
