@@ -62,8 +62,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-sample", type=int, default=192)
     ap.add_argument("--no-copy-ceiling", action="store_true")
     ap.add_argument("--unsplit", action="store_true", help="pipe5: ipp_pipe_hpass + full-frame ipp_pipe_vblend")
-    ap.add_argument("--split", action="store_true",
-                    help="pipe5: ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands (two launches) instead of ipp_pipe_fused")
+    ap.add_argument("--fused", action="store_true",
+                    help="pipe5: the one-launch ipp_pipe_fused instead of ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands "
+                         "(the two-launch split form, the default: measured 1-2 %% faster on MI355X, DESIGN.md §3)")
+    ap.add_argument("--split", action="store_true", help="pipe5: the split form (the default; kept for scripts)")
     ap.add_argument("--stream", action="store_true",
                     help="pipe5: also run the streaming form (a new plan per batch, planned on a host thread "
                          "while the previous batch runs) and report it beside the resident step")
@@ -302,7 +304,7 @@ def main(argv=None):
             runner = fused.PipeRunner(plan, dev)
             setup["taps_device_ms"] = round((time.perf_counter() - t_host) * 1e3, 1)
             setup["taps_host_tiles"] = runner.host_tiles
-            if runner.split and not args.unsplit and not args.split:
+            if runner.split and not args.unsplit and args.fused:
                 # one launch: H pass, background copy, V pass + paste (ipp_pipe_fused)
                 algo = {"ipp_pipe_fused": plan.algo_bytes_hpass_bgcopy + plan.algo_bytes_vblend_bands}
                 launches = [("ipp_pipe_fused", lambda: runner.fused(src, bgs, out))]

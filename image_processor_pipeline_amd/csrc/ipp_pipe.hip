@@ -476,6 +476,13 @@ __device__ __forceinline__ void paste_bands(const ipp_paste_desc& p, int& vb0, i
     vb1 = max(vb1, vb0);
 }
 
+// 16-B vectors per thread in flight in the background copy (IPP_COPY_U
+// overrides it in experiment builds).  A copy block holds one of the CU's
+// four H-pass block slots for as long as it streams, so bytes in flight per
+// block set how much H-pass time the copy displaces.
+#ifndef IPP_COPY_U
+#define IPP_COPY_U 16
+#endif
 template <int NT = 256>
 __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, const uint8_t* __restrict__ bg,
                                                       uint8_t* __restrict__ dst, int share, int nshare) {
@@ -494,15 +501,16 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4* s4 = reinterpret_cast<const u32x4*>(sb);
         u32x4* d4 = reinterpret_cast<u32x4*>(db);
-        for (int64_t i0 = a + threadIdx.x; i0 < e; i0 += 8 * NT) {
-            u32x4 v[8];
+        constexpr int U = IPP_COPY_U;
+        for (int64_t i0 = a + threadIdx.x; i0 < e; i0 += U * NT) {
+            u32x4 v[U];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < U; ++j) {
                 const int64_t i = i0 + NT * j;
                 if (i < e) v[j] = s4[i < n0 ? i : i + skip];
             }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < U; ++j) {
                 const int64_t i = i0 + NT * j;
                 if (i < e) __builtin_nontemporal_store(v[j], d4 + (i < n0 ? i : i + skip));
             }
@@ -673,7 +681,10 @@ constexpr int kVbX = 0;
 // orow (the band's unpremultiplied overlay rows in LDS) is indexed by
 // composite column - (p.x & ~15), so a 16-pixel composite group reads its 16
 // overlay pixels with four aligned ds_read_b128; the ≤ 15 columns before the
-// overlay and after it are zero (α 0: the background stays).
+// overlay and after it are zero (α 0: the background stays).  (A
+// quarter-planar layout that makes those reads conflict-free measured 0 on
+// the split V pass and -0.5 % on the fused launch, and spilled in one fused
+// instantiation: not kept.)
 __host__ __device__ constexpr int orow_stride(int ov_w_max) { return (ov_w_max + 32 + 3) & ~3; }
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -924,12 +935,30 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
 // ---------------------------------------------------------------------------
 constexpr int FUSE_LAG = 4;  // items between an item's H blocks and its V bands
 
+// The fused launch's LDS: an H block's ring and tables, or a V band's
+// unpremultiplied overlay rows (VBR × orow_stride(ov_w_max) words, at most
+// the H pass's size: ov_w_max ≤ ≈ 550 px; wider overlays take the split form).
+template <int NR>
+struct FusedLds {
+    union {
+        Hpass2Lds<NR> h;
+        uint32_t orow[sizeof(Hpass2Lds<NR>) / 4];
+    };
+    int32_t ready;
+};
+
+// (5-6 zoned ranges: 3 waves per SIMD too — at 4 the 3-channel form spilled
+// one register, and nothing may spill in a kernel with hand-waited gathers.)
 template <int NR, bool ZONES, int CN>
-__global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES && NR > 8 ? 3 : 4)))
+__global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES && NR > 4 ? 3 : 4)))
 k_pipe_fused(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
              const ipp_pipe_desc* __restrict__ descs, int n, int tyb, int cpi, int tyv, ipp_hsv_params hp,
              const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst, int ov_w_max, int32_t* __restrict__ sync) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // Static LDS: the H pass's table addresses then fold into the ds_read
+    // offset fields (through a dynamic region the compiler added the region's
+    // base to every table address: three v_add per gathered pixel).  The V
+    // bands' overlay rows share the region (the host checks they fit).
+    __shared__ FusedLds<NR> F;
     const uint32_t L = xcd_remap(blockIdx.x, gridDim.x);
     const int A = tyb + cpi, U = A + tyv, D = min(FUSE_LAG, n);
     // Block order: items 0..D-1 (H, copy); then per item i ≥ D: H(i), copy(i),
@@ -955,8 +984,7 @@ k_pipe_fused(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
             bg_copy_outside_bands<64 * HP_NW>(descs[im].p, bg, dst, k - tyb, cpi);
             return;
         }
-        hpass_block<NR, ZONES, CN, true>(*reinterpret_cast<Hpass2Lds<NR>*>(smem), src, tmp, coefs, descs, im, k, hp,
-                                         sync);
+        hpass_block<NR, ZONES, CN, true>(F.h, src, tmp, coefs, descs, im, k, hp, sync);
         return;
     }
     {
@@ -965,7 +993,7 @@ k_pipe_fused(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
         paste_bands(descs[im].p, vb0, vb1);
         if (vb0 + VBR * k >= vb1) return;
     }
-    __shared__ int32_t ready;
+    int32_t& ready = F.ready;
     if (threadIdx.x == 0) {
         const int need = (descs[im].h.lines + HR - 1) / HR;
         const int got = __hip_atomic_load(sync + im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -977,7 +1005,7 @@ k_pipe_fused(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const i
     }
     __syncthreads();
     if (!ready) return;
-    vblend_block<2, 0, true, true>(reinterpret_cast<uint32_t*>(smem), tmp, bg, dst, coefs, descs, im, k, ov_w_max);
+    vblend_block<2, 0, true, true>(F.orow, tmp, bg, dst, coefs, descs, im, k, ov_w_max);
 }
 
 // The bands queued by k_pipe_fused (after it: every H block has finished).
@@ -1009,10 +1037,17 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
     if (fz) {
         const int cpi = copy_blocks_per_item();
         const size_t vb = (size_t)VBR * orow_stride(fz->max_ov_w) * sizeof(uint32_t);
-        const size_t sm = std::max(sizeof(Hpass2Lds<NR>), vb);
+        if (vb > sizeof(Hpass2Lds<NR>)) {
+            // overlay rows wider than the fused launch's LDS: the split form
+            hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, true>), dim3((uint32_t)(n * (ty + cpi))), dim3(64 * HP_NW),
+                               0, s, src, tmp, coefs, descs, ty, hp, bg, dst, cpi);
+            hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 0, true>), dim3((uint32_t)(n * fz->tyv)), dim3(256), vb, s, tmp,
+                               bg, dst, coefs, descs, fz->tyv, fz->max_ov_w);
+            return;
+        }
         if (hipMemsetAsync(fz->sync, 0, (size_t)(n + 1) * sizeof(int32_t), s) != hipSuccess) return;
         hipLaunchKernelGGL((k_pipe_fused<NR, ZONES, CN>), dim3((uint32_t)(n * (ty + cpi + fz->tyv))),
-                           dim3(64 * HP_NW), sm, s, src, tmp, coefs, descs, n, ty, cpi, fz->tyv, hp, bg, dst,
+                           dim3(64 * HP_NW), 0, s, src, tmp, coefs, descs, n, ty, cpi, fz->tyv, hp, bg, dst,
                            fz->max_ov_w, fz->sync);
         hipLaunchKernelGGL(k_pipe_vdeferred, dim3((uint32_t)std::min(n * fz->tyv, 2048)), dim3(256), vb, s, tmp, bg,
                            dst, coefs, descs, n, fz->tyv, fz->max_ov_w, fz->sync);

@@ -33,6 +33,10 @@ from .device import SYM_FLIP, _stream, _to_dev
 
 ALL_SYMS = ("o", "h", "v", "hv")
 H_RING_COLUMNS = 512   # ipp_pipe.hip RING
+# Default launch form of a batch: "split" = ipp_pipe_hpass_bgcopy +
+# ipp_pipe_vblend_bands (measured 1-2 % faster on MI355X than the one-launch
+# "fused" = ipp_pipe_fused); both write the same bytes.
+PIPE_FORM = "split"
 
 
 @dataclass
@@ -363,8 +367,11 @@ class PipeRunner:
         for t, name in ((src, "src"), (bgs, "bgs"), (out, "out")):
             if not (t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous()):
                 raise N.NativeUnavailable(f"PipeRunner.run: {name} must be a contiguous uint8 ROCm tensor")
-        if self.split:
+        if self.split and PIPE_FORM == "fused":
             self.fused(src, bgs, out)
+        elif self.split:
+            self.hpass_bgcopy(src, bgs, out)
+            self.vblend_bands(bgs, out)
         else:
             self.hpass(src)
             self.vblend(bgs, out)
@@ -376,7 +383,7 @@ class PipeStream:
     own plan, built while the previous batch runs.  A worker thread runs
     batch k+1's host plan (ipp_plan_pipe_batch; ctypes drops the GIL) and
     its device taps (ipp_pipe_plan_taps on a side stream) while batch k's
-    fused launch runs on the caller's stream.  Device buffers live in
+    launches (PIPE_FORM) run on the caller's stream.  Device buffers live in
     `slots` sets that alternate; a set is refilled only after the batch that
     last used it has completed (its HIP event)."""
 
@@ -442,12 +449,24 @@ class PipeStream:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if record else None
                 if ev:
                     ev[0].record(main)
-                N.check(self.lib.ipp_pipe_fused(src.data_ptr(), b["tmp"].data_ptr(), b["coefs"].data_ptr(),
-                                                b["descs"].data_ptr(), len(plan.descs), plan.max_out_w,
-                                                plan.max_rows, 3, N.np_ptr(plan.hsv), plan.tap_format,
-                                                bgs.data_ptr(), out.data_ptr(), plan.bg_w, plan.bg_h,
-                                                plan.max_ov_w, plan.max_ov_h, b["sync"].data_ptr(),
-                                                main.cuda_stream), "ipp_pipe_fused")
+                if PIPE_FORM == "fused":
+                    N.check(self.lib.ipp_pipe_fused(src.data_ptr(), b["tmp"].data_ptr(), b["coefs"].data_ptr(),
+                                                    b["descs"].data_ptr(), len(plan.descs), plan.max_out_w,
+                                                    plan.max_rows, 3, N.np_ptr(plan.hsv), plan.tap_format,
+                                                    bgs.data_ptr(), out.data_ptr(), plan.bg_w, plan.bg_h,
+                                                    plan.max_ov_w, plan.max_ov_h, b["sync"].data_ptr(),
+                                                    main.cuda_stream), "ipp_pipe_fused")
+                else:
+                    N.check(self.lib.ipp_pipe_hpass_bgcopy(src.data_ptr(), b["tmp"].data_ptr(), b["coefs"].data_ptr(),
+                                                           b["descs"].data_ptr(), len(plan.descs), plan.max_out_w,
+                                                           plan.max_rows, 3, N.np_ptr(plan.hsv), plan.tap_format,
+                                                           bgs.data_ptr(), out.data_ptr(), main.cuda_stream),
+                            "ipp_pipe_hpass_bgcopy")
+                    N.check(self.lib.ipp_pipe_vblend_bands(b["tmp"].data_ptr(), bgs.data_ptr(), out.data_ptr(),
+                                                           b["coefs"].data_ptr(), b["descs"].data_ptr(),
+                                                           len(plan.descs), plan.bg_w, plan.bg_h, plan.max_ov_w,
+                                                           plan.max_ov_h, plan.tap_format, main.cuda_stream),
+                            "ipp_pipe_vblend_bands")
                 if ev:
                     ev[1].record(main)
                     self.events.append(ev)

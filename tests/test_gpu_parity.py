@@ -298,6 +298,51 @@ def test_pipe_fused_equals_split(D):
     print("bands queued for the second launch:", queued)
 
 
+def test_pipe_fused_wide_overlay_takes_split_form(D):
+    """Overlay rows wider than the fused launch's LDS (≈ 550 px) make
+    ipp_pipe_fused run the split kernels instead; the bytes are the same."""
+    from image_processor_pipeline_amd import fused
+    cfg = fused.PipeConfig(margins=(4, 4, 4, 4), scale_min=0.75, scale_max=0.8)
+    n, H, W, bh, bw = 2, 300, 260, 760, 800
+    rng = np.random.default_rng(11)
+    src = rng.integers(0, 256, (n, H, W, 3), np.uint8)
+    bgs = rng.integers(0, 256, (2, bh, bw, 3), np.uint8)
+    plan = fused.plan_pipe((H, W), n, (bh, bw), 2, cfg, seed=4)
+    assert plan.max_ov_w > 560
+    runner = fused.PipeRunner(plan, DEV)
+    a = torch.full((n, bh, bw, 3), 7, dtype=torch.uint8, device=DEV)
+    b = torch.full((n, bh, bw, 3), 9, dtype=torch.uint8, device=DEV)
+    runner.fused(_t(src), _t(bgs), a)
+    runner.hpass_bgcopy(_t(src), _t(bgs), b)
+    runner.vblend_bands(_t(bgs), b)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    got = a.cpu().numpy()
+    for i in range(n):
+        assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), i
+
+
+def test_pipe_stream_both_forms(D, monkeypatch):
+    """fused.PipeStream (bench.py --stream) in both launch forms: every batch
+    has its own plan; the last batch's output equals a PipeRunner run of the
+    same plan."""
+    from image_processor_pipeline_amd import fused
+    cfg = fused.PipeConfig(margins=(3, 5, 2, 7), scale_min=0.2, scale_max=0.6)
+    n, H, W, bh, bw = 6, 90, 110, 120, 160
+    rng = np.random.default_rng(21)
+    src = _t(rng.integers(0, 256, (n, H, W, 3), np.uint8))
+    bgs = _t(rng.integers(0, 256, (3, bh, bw, 3), np.uint8))
+    plan_fn = lambda k: fused.plan_pipe((H, W), n, (bh, bw), 3, cfg, seed=100 + k)
+    for form in ("split", "fused"):
+        monkeypatch.setattr(fused, "PIPE_FORM", form)
+        out = torch.empty((n, bh, bw, 3), dtype=torch.uint8, device=DEV)
+        fused.PipeStream(DEV, plan_fn).run(3, src, bgs, out, record=True)
+        ref = torch.empty_like(out)
+        fused.PipeRunner(plan_fn(2), DEV).run(src, bgs, ref)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), form
+
+
 def test_pipe_crop_reaching_source_end(D):
     """Zero bottom/right margins: the crop window ends at the source's last
     byte, so the last pixel's 4-byte gather would cross the image (and, for

@@ -2,7 +2,7 @@
 # Round-3 checkpoint session: the whole GPU suite (failures reported, the
 # session goes on unless the run itself died), smoke, the default bench line
 # with the streaming figure, the pipe5 kernel trace + PMC passes, then the
-# LDS-DMA semantics probe.  Every GPU step has its own time limit.
+# config-5 (video4k) line and profile when VIDEO is set.  Every GPU step has its own time limit.
 set -o pipefail
 TAG=${1:-r03g}
 mkdir -p gpurun_out
@@ -15,6 +15,6 @@ grep -E "FAILED|ERROR|passed|failed" gpurun_out/pytest_gpu_${TAG}.log | tail -15
 run 300 smoke_${TAG}.log python -c "import __graft_entry__ as g; g.smoke()"
 run 400 bench_${TAG}_pipe5.json.log python bench.py --stream
 bash tools/gpu_prof2.sh ${TAG}_pipe5 pipe5 4096 || exit 26
-run 60 lds_dma_probe_${TAG}.txt tools/probes/lds_dma_probe
-cat gpurun_out/lds_dma_probe_${TAG}.txt
+[ -n "$VIDEO" ] && run 400 bench_${TAG}_video4k.json.log python bench.py --workload video4k
+[ -n "$VIDEO" ] && { bash tools/gpu_prof2.sh ${TAG}_video4k video4k 256 || exit 27; }
 echo session done
