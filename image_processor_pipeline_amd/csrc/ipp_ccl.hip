@@ -383,7 +383,11 @@ __device__ __forceinline__ void tile_words(const uint8_t* __restrict__ img, cons
             if constexpr (SRC == SRC_ALPHA) {
                 fg = cur[kk] > 1u;
             } else {
-                uint32_t ex = hsv_tab_excl<NR, true>(*T, cur[kk]);
+                uint32_t ex;
+                if constexpr (!ZONES && HsvTables<NR>::kDecided)
+                    ex = hsv_tab_excl_vfirst<NR, true>(*T, cur[kk]);  // rows decided by v skip s and h
+                else
+                    ex = hsv_tab_excl<NR, true>(*T, cur[kk]);
                 if (ZONES) {
                     uint32_t zy = 0;
 #pragma unroll
