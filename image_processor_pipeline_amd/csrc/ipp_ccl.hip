@@ -407,6 +407,67 @@ __device__ __forceinline__ void tile_words(const uint8_t* __restrict__ img, cons
     p = lane > 0 ? p : 0ull;
 }
 
+// DPP move within 16-lane rows (row_shl:k, lanes past the row end read 0).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+// Mask words of one interior tile of a 3-channel HSV source (FULL): lane =
+// (row rr = lane >> 4 of a 4-row group, pixel quad q = lane & 15), one 12-byte
+// load per lane and group = 4 pixels (768 contiguous bytes per row group and
+// wave instruction, a quarter of the one-dword-per-lane loads of
+// tile_words).  The four fg bits of a lane form a nibble; a 16-lane DPP
+// reduction assembles each row's 64-bit word in lane 16·rr, which is moved
+// to lane r by readlane/writelane.  Same words as tile_words.
+template <int NR>
+__device__ __forceinline__ void tile_words_quads(const uint8_t* __restrict__ img, const ipp_image_desc& d, int X0,
+                                                 int y0, int lane, const HsvTables<NR>* T, u64& m, u64& p) {
+    struct u32x3 {
+        uint32_t x, y, z;
+    };  // 4-byte aligned: one global_load_dwordx3
+    const int q = lane & 15, rr = lane >> 4;
+    const uint8_t* base = img + d.off + (int64_t)(y0 + rr) * d.pitch + 3 * (X0 + 4 * q);
+    const int64_t gstep = 4 * (int64_t)d.pitch;  // next 4-row group
+    constexpr int G = TH / 4, GB = 4;             // 16 groups, loaded 4 at a time (double-buffered)
+    u32x3 bufA[GB], bufB[GB];
+#pragma unroll
+    for (int j = 0; j < GB; ++j) bufA[j] = *reinterpret_cast<const u32x3*>(base + j * gstep);
+    uint32_t mlo = 0u, mhi = 0u;
+#pragma unroll
+    for (int gb = 0; gb < G / GB; ++gb) {
+        u32x3(&cur)[GB] = (gb & 1) ? bufB : bufA;
+        u32x3(&nxt)[GB] = (gb & 1) ? bufA : bufB;
+        if (gb + 1 < G / GB) {
+#pragma unroll
+            for (int j = 0; j < GB; ++j) nxt[j] = *reinterpret_cast<const u32x3*>(base + ((gb + 1) * GB + j) * gstep);
+        }
+#pragma unroll
+        for (int j = 0; j < GB; ++j) {
+            const uint32_t w0 = cur[j].x, w1 = cur[j].y, w2 = cur[j].z;
+            const uint32_t px[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 3), __builtin_amdgcn_alignbyte(w2, w1, 2),
+                                    w2 >> 8};
+            uint32_t nib = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) nib |= (hsv_tab_excl_vfirst<NR, true>(*T, px[k]) == 0u ? 1u : 0u) << k;
+            // lanes 16rr + q → lane 16rr: 4 → 8 → 16 → 32 bits, then the high half
+            uint32_t t = nib | (dpp<0x101>(nib) << 4);      // row_shl:1
+            t = t | (dpp<0x102>(t) << 8);                     // row_shl:2
+            t = t | (dpp<0x104>(t) << 16);                    // row_shl:4
+            const uint32_t hi = dpp<0x108>(t);                // row_shl:8: bits 32..63
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const int r = 4 * (gb * GB + j) + r4;
+                writelane(mlo, (uint32_t)__builtin_amdgcn_readlane((int)t, 16 * r4), r);
+                writelane(mhi, (uint32_t)__builtin_amdgcn_readlane((int)hi, 16 * r4), r);
+            }
+        }
+    }
+    m = ((u64)mhi << 32) | mlo;
+    p = __shfl_up(m, 1);
+    p = lane > 0 ? p : 0ull;
+}
+
 // K1: one wave per 64×64 tile, WAVES tiles side by side per block.
 #ifndef IPP_CCL_WPE  // K1 occupancy target (waves per SIMD; 0 = the compiler's choice): 6 → 49-55 VGPRs, 7 waves/SIMD, no spills; 3.44 vs 3.63 ms per video4k step (the default choice was 85-89 VGPRs, 5 waves)
 #define IPP_CCL_WPE 6
@@ -450,7 +511,12 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
     u64 m, p;
     const HsvTables<NR>* Tp = nullptr;
     if constexpr (SRC == SRC_HSV) Tp = &T;
-    if (X0 + TW <= d.w && y0 + TH < d.h)
+    if constexpr (SRC == SRC_HSV && !ZONES && HsvTables<NR>::kDecided) {
+        if (X0 + TW <= d.w && y0 + TH <= d.h)
+            tile_words_quads<NR>(img, d, X0, y0, lane, Tp, m, p);
+        else
+            tile_words<SRC, NR, ZONES, false>(img, d, x, y0, lane, Tp, R, m, p);
+    } else if (X0 + TW <= d.w && y0 + TH < d.h)
         tile_words<SRC, NR, ZONES, true>(img, d, x, y0, lane, Tp, R, m, p);
     else
         tile_words<SRC, NR, ZONES, false>(img, d, x, y0, lane, Tp, R, m, p);

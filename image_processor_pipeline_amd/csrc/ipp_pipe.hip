@@ -654,12 +654,23 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
     // blocks followed by cpi background-copy blocks, so the copies run beside
     // the H pass on every XCD.
     const int per_item = tiles_y + (COPY ? cpi : 0);
+#if defined(IPP_DIAG) && defined(IPP_DIAG_COPY_LAST)
+    // diagnostic block order: every H block first, then every copy block
+    const int nimg = gridDim.x / per_item;
+    int im, tb;
+    if (b < (uint32_t)(nimg * tiles_y)) { im = b / tiles_y; tb = b - im * tiles_y; }
+    else { const int c = b - nimg * tiles_y; im = c / cpi; tb = tiles_y + c - im * cpi; }
+#else
     const int im = b / per_item;
     const int tb = b - im * per_item;
+#endif
     if (COPY && tb >= tiles_y) {
         bg_copy_outside_bands<64 * HP_NW>(descs[im].p, bg, dst, tb - tiles_y, cpi);
         return;
     }
+#if defined(IPP_DIAG) && defined(IPP_DIAG_COPY_ONLY)
+    return;  // diagnostic (wrong output): the copy blocks alone
+#endif
     hpass_block<NR, ZONES, CN, false>(L, src, tmp, coefs, descs, im, tb, hp, nullptr);
 }
 
@@ -1053,14 +1064,20 @@ void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, co
                            dst, coefs, descs, n, fz->tyv, fz->max_ov_w, fz->sync);
         return;
     }
+#ifdef IPP_DIAG
+    // diagnostic: unused dynamic LDS per block, to cap the blocks per CU
+    static const size_t pad = (size_t)diag_env("IPP_HP_PAD", 0);
+#else
+    constexpr size_t pad = 0;
+#endif
     if (bg && dst) {  // H pass + the background rows outside the overlay bands
         const int cpi = copy_blocks_per_item();
-        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, true>), dim3((uint32_t)(n * (ty + cpi))), dim3(64 * HP_NW), 0,
-                           s, src, tmp, coefs, descs, ty, hp, bg, dst, cpi);
+        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, true>), dim3((uint32_t)(n * (ty + cpi))), dim3(64 * HP_NW),
+                           pad, s, src, tmp, coefs, descs, ty, hp, bg, dst, cpi);
         return;
     }
-    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, false>), grid, dim3(64 * HP_NW), 0, s, src, tmp, coefs, descs, ty,
-                       hp, bg, dst, 0);
+    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, false>), grid, dim3(64 * HP_NW), pad, s, src, tmp, coefs, descs,
+                       ty, hp, bg, dst, 0);
 }
 
 template <int NR>

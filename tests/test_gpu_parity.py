@@ -513,6 +513,28 @@ def test_video_chain_noise_frames_vs_oracle(D):
             assert res[i] is not None and np.array_equal(res[i], exp), (h, w, i)
 
 
+def test_video_chain_random_colour_frames_vs_oracle(D):
+    """Uniform random BGR frames: every HSV path (v alone decides, full
+    saturation / hue test) on every pixel position of the 4-pixels-per-lane
+    loader, with heights that are multiples of 64 (the last tile row takes
+    that loader too) and off-grid ones.  The kept share percolates, so the
+    largest component spans the frame and the crop's α checks almost every
+    foreground bit."""
+    from image_processor_pipeline_amd import geometry as G
+    from image_processor_pipeline_amd.video_chain import VideoChain
+    rng = np.random.default_rng(8)
+    for (h, w) in [(256, 320), (192, 448), (200, 330)]:
+        n = 2
+        fr = rng.integers(0, 256, (n, h, w, 3), np.uint8)
+        chain = VideoChain(n, h, w, DEV)
+        chain.run(_t(fr))
+        res = chain.results()
+        for i in range(n):
+            exp = ops.keep_largest_component(ops.color_mask_bgra(fr[i], G.REFERENCE_HSV_RANGES))
+            assert res[i] is not None and np.array_equal(res[i], exp), (h, w, i)
+            assert res[i].shape[0] * res[i].shape[1] > 0.5 * h * w
+
+
 # --------------------------------------------------------------------------- config 5: 4K video chain
 
 def test_video_chain_4k_vs_oracle(D):

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Quick A/B session: pipe parity tests, then bench lines for the given
-# variants: "[<variant library>|]<bench.py args>" (a library path runs that
-# experiment build through IPP_LIB_PATH).  tools/gpu_ab.sh <tag> "<A>" "<B>" ...
+# variants: "[<variant library>[@VAR=val,...]|]<bench.py args>" (a library path
+# runs that experiment build through IPP_LIB_PATH; @ exports its env vars).  tools/gpu_ab.sh <tag> "<A>" "<B>" ...
 set -o pipefail
 TAG=$1; shift
 mkdir -p gpurun_out
@@ -10,10 +10,11 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_be
 tail -1 gpurun_out/pt_${TAG}.log
 i=0
 for a in "$@"; do
-  lib=""; args="$a"
+  lib=""; args="$a"; envs=""
   case "$a" in *"|"*) lib="${a%%|*}"; args="${a#*|}";; esac
+  case "$lib" in *"@"*) envs="${lib#*@}"; lib="${lib%%@*}";; esac
   if [ -n "$lib" ]; then export IPP_LIB_PATH=$lib; else unset IPP_LIB_PATH; fi
-  timeout -k 10 300 python bench.py --no-cpu-baseline $args > gpurun_out/bench_${TAG}_$i.json.log 2>&1 || { tail -20 gpurun_out/bench_${TAG}_$i.json.log; exit 22; }
+  timeout -k 10 300 env ${envs//,/ } python bench.py --no-cpu-baseline $args > gpurun_out/bench_${TAG}_$i.json.log 2>&1 || { tail -20 gpurun_out/bench_${TAG}_$i.json.log; exit 22; }
   python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'], d['value'], d['kernels_ms'])" gpurun_out/bench_${TAG}_$i.json.log "$a"
   i=$((i+1))
 done
