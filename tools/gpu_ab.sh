@@ -6,7 +6,7 @@ set -o pipefail
 TAG=$1; shift
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_benchscale.py -k "pipe or benchscale" -x -q --timeout 240 --timeout-method thread > gpurun_out/pt_${TAG}.log 2>&1 || { tail -30 gpurun_out/pt_${TAG}.log; exit 21; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_benchscale.py tests/test_transforms_gpu.py -k "${PT:-pipe or benchscale}" -x -q --timeout 240 --timeout-method thread > gpurun_out/pt_${TAG}.log 2>&1 || { tail -30 gpurun_out/pt_${TAG}.log; exit 21; }
 tail -1 gpurun_out/pt_${TAG}.log
 i=0
 for a in "$@"; do
