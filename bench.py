@@ -69,6 +69,8 @@ def parse(argv=None):
     ap.add_argument("--stream", action="store_true",
                     help="pipe5: also run the streaming form (a new plan per batch, planned on a host thread "
                          "while the previous batch runs) and report it beside the resident step")
+    ap.add_argument("--stream-default-priority", action="store_true",
+                    help="--stream: launch the pipe on the default-priority stream (not a high-priority one)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: CPU rehearsal of the N-rank path (tests)")
     ap.add_argument("--dump-digests", default=None,
@@ -432,7 +434,7 @@ def main(argv=None):
         # planned on a worker thread (host planner + device taps on a side
         # stream) while batch k-1 runs.  The clock starts with the pipeline
         # primed and stops when the last batch has finished.
-        ps = fused.PipeStream(dev, plan_batch)
+        ps = fused.PipeStream(dev, plan_batch, priority=not args.stream_default_priority)
         clock = {}
 
         def mark():

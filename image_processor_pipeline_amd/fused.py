@@ -387,11 +387,16 @@ class PipeStream:
     `slots` sets that alternate; a set is refilled only after the batch that
     last used it has completed (its HIP event)."""
 
-    def __init__(self, device, plan_fn, slots: int = 2):
+    def __init__(self, device, plan_fn, slots: int = 2, priority: bool = True):
         self.device = torch.device(device)
         self.plan_fn = plan_fn                  # batch index -> PipePlan
         self.lib = N.load()
         self.side = torch.cuda.Stream(self.device)
+        # The pipe launches go to a high-priority stream (the hardware queue
+        # dispatches its blocks first): the tap planner of the next batch, on
+        # the default-priority side stream, then fills the CU slots the pipe
+        # leaves free instead of displacing H-pass blocks.
+        self.main = torch.cuda.Stream(self.device, priority=-1) if priority else None
         self.slots = [{"done": torch.cuda.Event(), "bufs": {}} for _ in range(max(2, slots))]
         self.timing: List[Tuple[float, float, int]] = []   # per batch: host plan ms, taps ms, host tiles
         self.events: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []
@@ -436,7 +441,9 @@ class PipeStream:
         launched, with the pipeline primed (its plan ready, the next one not
         yet started) — bench.py starts its clock there."""
         from concurrent.futures import ThreadPoolExecutor
-        main = torch.cuda.current_stream(self.device)
+        main = self.main if self.main is not None else torch.cuda.current_stream(self.device)
+        if self.main is not None:
+            self.main.wait_stream(torch.cuda.current_stream(self.device))  # inputs written on the caller's stream
         with ThreadPoolExecutor(1) as ex:
             fut = ex.submit(self._prepare, 0, self.slots[0])
             for k in range(n_batches):
@@ -472,3 +479,5 @@ class PipeStream:
                     self.events.append(ev)
                 slot["done"].record(main)
                 self.timing.append(tm)
+        if self.main is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.main)  # outputs visible to the caller's stream

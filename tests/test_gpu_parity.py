@@ -333,10 +333,10 @@ def test_pipe_stream_both_forms(D, monkeypatch):
     src = _t(rng.integers(0, 256, (n, H, W, 3), np.uint8))
     bgs = _t(rng.integers(0, 256, (3, bh, bw, 3), np.uint8))
     plan_fn = lambda k: fused.plan_pipe((H, W), n, (bh, bw), 3, cfg, seed=100 + k)
-    for form in ("split", "fused"):
+    for form, prio in (("split", True), ("fused", True), ("split", False)):
         monkeypatch.setattr(fused, "PIPE_FORM", form)
         out = torch.empty((n, bh, bw, 3), dtype=torch.uint8, device=DEV)
-        fused.PipeStream(DEV, plan_fn).run(3, src, bgs, out, record=True)
+        fused.PipeStream(DEV, plan_fn, priority=prio).run(3, src, bgs, out, record=True)
         ref = torch.empty_like(out)
         fused.PipeRunner(plan_fn(2), DEV).run(src, bgs, ref)
         torch.cuda.synchronize()
