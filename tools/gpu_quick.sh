@@ -9,5 +9,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout
 tail -1 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 22; }
 echo smoke ok
-timeout -k 10 600 python bench.py > gpurun_out/bench_${TAG}_pipe5.json.log 2>&1 || { tail -20 gpurun_out/bench_${TAG}_pipe5.json.log; exit 23; }
+timeout -k 10 600 python bench.py --stream > gpurun_out/bench_${TAG}_pipe5.json.log 2>&1 || { tail -20 gpurun_out/bench_${TAG}_pipe5.json.log; exit 23; }
 tail -1 gpurun_out/bench_${TAG}_pipe5.json.log
