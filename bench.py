@@ -66,9 +66,6 @@ def parse(argv=None):
                     help="pipe5: the one-launch ipp_pipe_fused instead of ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands "
                          "(the two-launch split form, the default: measured 1-2 %% faster on MI355X, DESIGN.md §3)")
     ap.add_argument("--split", action="store_true", help="pipe5: the split form (the default; kept for scripts)")
-    ap.add_argument("--overlap-copy", action="store_true",
-                    help="pipe5 (experiment): ipp_pipe_hpass on the main stream beside ipp_pipe_bgcopy (one-wave "
-                         "blocks) on a side stream, then ipp_pipe_vblend_bands")
     ap.add_argument("--stream", action="store_true",
                     help="pipe5: also run the streaming form (a new plan per batch, planned on a host thread "
                          "while the previous batch runs) and report it beside the resident step")
@@ -309,24 +306,7 @@ def main(argv=None):
             runner = fused.PipeRunner(plan, dev)
             setup["taps_device_ms"] = round((time.perf_counter() - t_host) * 1e3, 1)
             setup["taps_host_tiles"] = runner.host_tiles
-            if runner.split and args.overlap_copy:
-                side = torch.cuda.Stream(dev)
-                ev_go, ev_copied = torch.cuda.Event(), torch.cuda.Event()
-                ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-
-                def hpass_overlapped():
-                    main = torch.cuda.current_stream(dev)
-                    ev_go.record(main)
-                    side.wait_event(ev_go)
-                    runner.bgcopy(bgs, out, side, 4 * ncu)      # one wave per SIMD, launched first
-                    runner.hpass(src)
-                    ev_copied.record(side)
-                    main.wait_event(ev_copied)
-                algo = {"ipp_pipe_hpass+bgcopy": plan.algo_bytes_hpass_bgcopy,
-                        "ipp_pipe_vblend_bands": plan.algo_bytes_vblend_bands}
-                launches = [("ipp_pipe_hpass+bgcopy", hpass_overlapped),
-                            ("ipp_pipe_vblend_bands", lambda: runner.vblend_bands(bgs, out))]
-            elif runner.split and not args.unsplit and args.fused:
+            if runner.split and not args.unsplit and args.fused:
                 # one launch: H pass, background copy, V pass + paste (ipp_pipe_fused)
                 algo = {"ipp_pipe_fused": plan.algo_bytes_hpass_bgcopy + plan.algo_bytes_vblend_bands}
                 launches = [("ipp_pipe_fused", lambda: runner.fused(src, bgs, out))]

@@ -119,7 +119,6 @@ _L = ctypes.c_int64
 _D = ctypes.c_double
 SIGNATURES = {
     "ipp_rotate_flip_nearest": (_I, [_P, _P, _P, _I, _I, _I, _P]),
-    "ipp_pipe_bgcopy": (_I, [_P, _I, _P, _P, _I, _P]),
     "ipp_rotate_bilinear": (_I, [_P, _P, _P, _I, _I, _I, _P]),
     "ipp_copy_window": (_I, [_P, _P, _P, _I, _I, _I, _P]),
     "ipp_crop_to_bbox": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),

@@ -534,20 +534,6 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
     }
 }
 
-// Background copy as its own low-footprint launch (experiment): one-wave
-// blocks, ≤ 32 VGPRs, persistent over (item, share) units, meant to run on a
-// second stream beside an H pass of ≤ 120 VGPRs so that it takes no H-pass
-// block slot (4 × 120 + 32 = 512 registers per SIMD lane).
-constexpr int BGC_SHARES = 16;  // work units per item
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(32)))
-k_bg_copy_persist(const ipp_pipe_desc* __restrict__ descs, int n, const uint8_t* __restrict__ bg,
-                  uint8_t* __restrict__ dst) {
-    for (int u = blockIdx.x; u < n * BGC_SHARES; u += gridDim.x) {
-        const int im = u / BGC_SHARES;
-        bg_copy_outside_bands<64, 3>(descs[im].p, bg, dst, u - im * BGC_SHARES, BGC_SHARES);
-    }
-}
-
 // One H-pass block: band tb of item im.  SYNC (fused launch): T is stored
 // write-through and, once every wave's stores have drained, the block adds one
 // to the item's completion counter (agent scope) — the hand-off protocol of
@@ -643,13 +629,9 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
     // Fill value (raw 0): uniform over the block except for zone bits.
     const uint32_t fill = hsv2_px<NR, ZONES>(L.T, 0u, ~0u);
     const int nrows = min(HR, h.lines - row0);
-#if defined(IPP_DIAG) && defined(IPP_DIAG_NOCLAMP)
-    (void)clamp;  // diagnostic (wrong for items whose last pixel's dword crosses the image end)
-#else
     if (CN == 3 && clamp)
         hpass2_body<NR, ZONES, CN, true, SYNC>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
     else
-#endif
         hpass2_body<NR, ZONES, CN, false, SYNC>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
     if (SYNC) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's T stores have reached memory
@@ -1196,16 +1178,6 @@ extern "C" int ipp_pipe_fused(const uint8_t* src, uint8_t* tmp, const int32_t* c
     const FusedCfg fz{fused_tyv(bg_h, max_ov_h), max_ov_w, reinterpret_cast<int32_t*>(sync)};
     return pipe_hpass_impl(src, tmp, coefs, descs, n_images, max_out_w, max_rows, src_cn, hsv, tap_format, bg, dst,
                            stream, &fz);
-}
-
-extern "C" int ipp_pipe_bgcopy(const ipp_pipe_desc* descs, int32_t n_images, const uint8_t* bg, uint8_t* dst,
-                               int32_t n_blocks, void* stream) {
-    if (n_images == 0) return IPP_OK;
-    if (!descs || !bg || !dst || n_images < 0 || n_blocks <= 0) return IPP_E_ARG;
-    hipLaunchKernelGGL(k_bg_copy_persist, dim3((uint32_t)n_blocks), dim3(64), 0, (hipStream_t)stream, descs, n_images,
-                       bg, dst);
-    IPP_CHECK_LAUNCH();
-    return IPP_OK;
 }
 
 extern "C" int ipp_pipe_status(int32_t* status, void* stream) {

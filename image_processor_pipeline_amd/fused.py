@@ -328,13 +328,6 @@ class PipeRunner:
                                                N.np_ptr(p.hsv), p.tap_format, bgs.data_ptr(), out.data_ptr(),
                                                _stream(self.device)), "ipp_pipe_hpass_bgcopy")
 
-    def bgcopy(self, bgs: torch.Tensor, out: torch.Tensor, stream, n_blocks: int) -> None:
-        """The composite rows outside the overlay bands as a launch of its own
-        (ipp_pipe_bgcopy) on `stream`: n_blocks one-wave persistent blocks."""
-        p = self.plan
-        N.check(self.lib.ipp_pipe_bgcopy(self.descs.data_ptr(), len(p.descs), bgs.data_ptr(), out.data_ptr(),
-                                         n_blocks, stream.cuda_stream), "ipp_pipe_bgcopy")
-
     def vblend_bands(self, bgs: torch.Tensor, out: torch.Tensor) -> None:
         """V pass + paste over the 16-row bands the overlay touches (split form)."""
         p = self.plan

@@ -247,12 +247,6 @@ int ipp_pipe_hpass_bgcopy(const uint8_t* src, uint8_t* tmp, const int32_t* coefs
                           int32_t max_out_w, int32_t max_rows, int32_t src_cn,
                           const ipp_hsv_params* hsv, int32_t tap_format,
                           const uint8_t* bg, uint8_t* dst, void* stream);
-/* The composite rows outside the overlay bands (overlays.py:138-139 leaves
- * them as the background) as a launch of its own: n_blocks one-wave blocks,
- * persistent, few registers, for a second stream beside ipp_pipe_hpass. */
-int ipp_pipe_bgcopy(const ipp_pipe_desc* descs, int32_t n_images, const uint8_t* bg, uint8_t* dst,
-                    int32_t n_blocks, void* stream);
-
 int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
                           const int32_t* coefs, const ipp_pipe_desc* descs, int32_t n_images,
                           int32_t bg_w, int32_t bg_h, int32_t max_ov_w, int32_t max_ov_h,
