@@ -653,16 +653,8 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
     // blocks followed by cpi background-copy blocks, so the copies run beside
     // the H pass on every XCD.
     const int per_item = tiles_y + (COPY ? cpi : 0);
-#if defined(IPP_DIAG) && defined(IPP_DIAG_COPY_LAST)
-    // diagnostic block order: every H block first, then every copy block
-    const int nimg = gridDim.x / per_item;
-    int im, tb;
-    if (b < (uint32_t)(nimg * tiles_y)) { im = b / tiles_y; tb = b - im * tiles_y; }
-    else { const int c = b - nimg * tiles_y; im = c / cpi; tb = tiles_y + c - im * cpi; }
-#else
     const int im = b / per_item;
     const int tb = b - im * per_item;
-#endif
     if (COPY && tb >= tiles_y) {
         bg_copy_outside_bands<64 * HP_NW>(descs[im].p, bg, dst, tb - tiles_y, cpi);
         return;
