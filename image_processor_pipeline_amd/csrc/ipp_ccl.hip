@@ -447,20 +447,24 @@ __device__ __forceinline__ void tile_words_quads(const uint8_t* __restrict__ img
             const uint32_t w0 = cur[j].x, w1 = cur[j].y, w2 = cur[j].z;
             const uint32_t px[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 3), __builtin_amdgcn_alignbyte(w2, w1, 2),
                                     w2 >> 8};
+            HsvPre pre[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) pre[k] = hsv_pre<NR, true>(*T, px[k]);
             uint32_t nib = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) nib |= (hsv_tab_excl_vfirst<NR, true>(*T, px[k]) == 0u ? 1u : 0u) << k;
+            for (int k = 0; k < 4; ++k) nib |= (hsv_post<NR>(*T, pre[k]) == 0u ? 1u : 0u) << k;
             // lanes 16rr + q → lane 16rr: 4 → 8 → 16 → 32 bits, then the high half
             uint32_t t = nib | (dpp<0x101>(nib) << 4);      // row_shl:1
             t = t | (dpp<0x102>(t) << 8);                     // row_shl:2
             t = t | (dpp<0x104>(t) << 16);                    // row_shl:4
             const uint32_t hi = dpp<0x108>(t);                // row_shl:8: bits 32..63
-#pragma unroll
-            for (int r4 = 0; r4 < 4; ++r4) {
-                const int r = 4 * (gb * GB + j) + r4;
-                writelane(mlo, (uint32_t)__builtin_amdgcn_readlane((int)t, 16 * r4), r);
-                writelane(mhi, (uint32_t)__builtin_amdgcn_readlane((int)hi, 16 * r4), r);
-            }
+            // lanes 4G..4G+3 (G = this group) take the words of lanes 0, 16, 32, 48
+            const int src = 64 * (lane & 3);                  // ds_bpermute byte address of lane 16·(lane & 3)
+            const uint32_t wlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)t);
+            const uint32_t whi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)hi);
+            const bool mine = (lane >> 2) == gb * GB + j;
+            mlo = mine ? wlo : mlo;
+            mhi = mine ? whi : mhi;
         }
     }
     m = ((u64)mhi << 32) | mlo;
