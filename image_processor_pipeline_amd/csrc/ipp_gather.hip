@@ -18,6 +18,7 @@
 namespace {
 
 constexpr int TILE_W = 64, TILE_H = 16, PX_PER_THREAD = 4;
+constexpr int STAGE_W = 72;  // words per restaged row (dense map)
 
 struct TileGrid {
     int tiles_x, tiles_y;
@@ -78,14 +79,16 @@ __device__ __forceinline__ void rotate_tiles(const uint8_t* __restrict__ src, ui
         int sy = (ty0 + r) * TILE_H + gy, sx0 = x0;
         if (DENSE) {  // restage pixel by pixel: store pattern = ROWS map
             if (r > 0) __syncthreads();
+            // rows STAGE_W words apart: the 4 rows × 8 columns of a half-wave's
+            // dword writes land on 32 distinct banks (64 words: 4-way conflicts)
             uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);
-            st32[gy * 64 + gx] = px.x;
-            st32[gy * 64 + gx + 8] = px.y;
-            st32[(gy + 8) * 64 + gx] = px.z;
-            st32[(gy + 8) * 64 + gx + 8] = px.w;
+            st32[gy * STAGE_W + gx] = px.x;
+            st32[gy * STAGE_W + gx + 8] = px.y;
+            st32[(gy + 8) * STAGE_W + gx] = px.z;
+            st32[(gy + 8) * STAGE_W + gx + 8] = px.w;
             __syncthreads();
             const int ry = (int)(threadIdx.x >> 4), rx = 4 * (int)(threadIdx.x & 15);
-            px = stage[ry * 16 + (rx >> 2)];
+            px = stage[ry * (STAGE_W / 4) + (rx >> 2)];
             sy = (ty0 + r) * TILE_H + ry;
             sx0 = tx * TILE_W + rx;
         } else if (PATCH) {  // restage: store pattern = ROWS map
@@ -113,7 +116,7 @@ template <bool PATCH, bool DENSE = false>
 __global__ void __launch_bounds__(256)
 k_rotate_flip_nearest(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                       const ipp_gather_desc* __restrict__ descs, int tiles_x, int tiles_y) {
-    __shared__ uint4 stage[PATCH || DENSE ? TILE_H * 16 : 1];
+    __shared__ uint4 stage[PATCH || DENSE ? TILE_H * (STAGE_W / 4) : 1];
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int per_img = tiles_x * tiles_y;
     const int img = b / per_img;
