@@ -67,8 +67,11 @@ def parse(argv=None):
                          "(the two-launch split form, the default: measured 1-2 %% faster on MI355X, DESIGN.md §3)")
     ap.add_argument("--split", action="store_true", help="pipe5: the split form (the default; kept for scripts)")
     ap.add_argument("--stream", action="store_true",
-                    help="pipe5: also run the streaming form (a new plan per batch, planned on a host thread "
-                         "while the previous batch runs) and report it beside the resident step")
+                    help="pipe5: the streaming leg (the default; kept for scripts)")
+    ap.add_argument("--no-stream", action="store_true",
+                    help="pipe5: skip the streaming leg (a new plan per batch, planned on a host thread while the "
+                         "previous batch runs), which is otherwise timed after the resident step and reported "
+                         "beside it")
     ap.add_argument("--stream-default-priority", action="store_true",
                     help="--stream: launch the pipe on the default-priority stream (not a high-priority one)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -429,7 +432,7 @@ def main(argv=None):
         elapsed = float(t.item())
 
     stream_res = None
-    if args.stream and args.workload == "pipe5":
+    if not args.no_stream and args.workload == "pipe5":
         # Streaming: batch k of the timed run has its own plan (seed + k),
         # planned on a worker thread (host planner + device taps on a side
         # stream) while batch k-1 runs.  The clock starts with the pipeline

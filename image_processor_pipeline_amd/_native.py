@@ -22,7 +22,6 @@ IPP_E_ARG = -1
 IPP_E_LAUNCH = -2
 IPP_E_RANGE = -3
 IPP_MAX_HSV_RANGES = 16
-IPP_TAPS_DOT4 = 0
 IPP_TAPS_MFMA = 1
 IPP_RS_PREMULTIPLY = 1
 IPP_RS_UNPREMULTIPLY = 2
@@ -140,9 +139,6 @@ SIGNATURES = {
     "ipp_plan_lanczos_ksize": (_I, [_D, _D, _I]),
     "ipp_plan_lanczos_batch": (_I, [_I, _P, _P, _P, _P, _L, _I]),
     "ipp_plan_opaque_bbox": (_I, [_I, _I, _P, _I, _I, _P]),
-    "ipp_plan_dot4_stride": (_I, [_I]),
-    "ipp_plan_dot4_size": (_L, [_I, _I]),
-    "ipp_plan_dot4_from_taps": (_I, [_I, _I, _P, _I, _I, _P]),
     "ipp_plan_mfma_size": (_L, [_I, _I, _I]),
     "ipp_plan_mfma_from_taps": (_I, [_I, _I, _I, _P, _I, _I, _P]),
     "ipp_plan_mfma_nk_bound": (_I, [_I, _I, _I]),

@@ -423,9 +423,12 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
 template <int NR>
 __device__ __forceinline__ void tile_words_quads(const uint8_t* __restrict__ img, const ipp_image_desc& d, int X0,
                                                  int y0, int lane, const HsvTables<NR>* T, u64& m, u64& p) {
-    struct u32x3 {
+    // 12 bytes at a 3-byte pixel boundary: no alignment promise (the pitch
+    // 3·w and the image offset need not be multiples of 4); the queues run in
+    // unaligned-access mode, so this is still one global_load_dwordx3
+    struct __attribute__((packed, aligned(1), may_alias)) u32x3 {
         uint32_t x, y, z;
-    };  // 4-byte aligned: one global_load_dwordx3
+    };
     const int q = lane & 15, rr = lane >> 4;
     const uint8_t* base = img + d.off + (int64_t)(y0 + rr) * d.pitch + 3 * (X0 + 4 * q);
     const int64_t gstep = 4 * (int64_t)d.pitch;  // next 4-row group

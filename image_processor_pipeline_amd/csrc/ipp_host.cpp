@@ -185,18 +185,8 @@ extern "C" int ipp_plan_opaque_bbox(int32_t in_w, int32_t in_h, const int32_t a[
 
 extern "C" const char* ipp_version(void) { return "ipp 0.1.0 (gfx950)"; }
 
-// ---------------------------------------------------------------------------
-// dot4 tap format (fused pipe kernels).  For output o with Pillow taps
-// k[0..cnt) starting at input index xmin (optionally shifted by `shift`):
-//   hdr[o]    = (g0, ng, bias, 0)   g0 = (xmin-shift) & ~3 (4-aligned start),
-//                                   ng = ceil(((xmin-shift)&3) + cnt) / 4),
-//                                   bias = 2^21 + 128 * Σk
-//   planes[o][j] = (P0, P1, P2, 0)  byte b of Pp = balanced signed byte p of
-//                                   tap (4j + b - ((xmin-shift)&3))  (0 outside)
-// so that for pixels stored XOR 0x80 (i.e. p - 128 as int8):
-//   2^21 + Σ p·k = bias + Σ_p 2^(8p) · Σ_j sdot4(pix4_j, Pp_j)   exactly.
-// Layout per axis: hdr[out][4] then planes[out][ngs][4] (ngs = stride).
-// ---------------------------------------------------------------------------
+// Balanced signed bytes of a 22-bit tap: k = b0 + 256 b1 + 65536 b2, each
+// b in [-128, 127] (the MFMA tile format below).
 namespace {
 
 inline void balanced_bytes(int32_t k, int8_t b[3]) {
@@ -209,56 +199,6 @@ inline void balanced_bytes(int32_t k, int8_t b[3]) {
 }
 
 }  // namespace
-
-extern "C" int32_t ipp_plan_dot4_stride(int32_t ksize) { return (ksize + 3 + 3) / 4; }
-
-extern "C" int64_t ipp_plan_dot4_size(int32_t out_size, int32_t ksize) {
-    return 4ll * out_size + 4ll * out_size * ipp_plan_dot4_stride(ksize);
-}
-
-// Convert standard Pillow taps (bounds[2*out] + taps[out*ksize]) into the dot4
-// format; `shift` is subtracted from every xmin (the V pass's ybox_first).
-extern "C" int ipp_plan_dot4_from_taps(int32_t out_size, int32_t ksize, const int32_t* std_taps, int32_t shift,
-                                       int32_t transposed, int32_t* out) {
-    if (out_size <= 0 || ksize <= 0 || !std_taps || !out) return IPP_E_ARG;
-    const int ngs = ipp_plan_dot4_stride(ksize);
-    const int32_t* bounds = std_taps;
-    const int32_t* kk = std_taps + 2 * (int64_t)out_size;
-    int32_t* hdr = out;
-    int32_t* planes = out + 4 * (int64_t)out_size;
-    for (int o = 0; o < out_size; ++o) {
-        const int xmin = bounds[2 * o] - shift, cnt = bounds[2 * o + 1];
-        if (xmin < 0) return IPP_E_RANGE;
-        const int off = xmin & 3, g0 = xmin - off;
-        const int ng = (off + cnt + 3) / 4;
-        if (ng > ngs) return IPP_E_RANGE;
-        int64_t sum = 0;
-        // group j of output o lives at planes[(o*ngs + j)*4] (row-major) or
-        // planes[(j*out_size + o)*4] (transposed: a wave's lanes read 16 B each,
-        // contiguous, for one j).
-        auto grp = [&](int j) -> int32_t* {
-            return planes + 4 * (transposed ? ((int64_t)j * out_size + o) : ((int64_t)o * ngs + j));
-        };
-        for (int j = 0; j < ngs; ++j) {
-            int32_t* pl = grp(j);
-            pl[0] = pl[1] = pl[2] = pl[3] = 0;
-        }
-        for (int t = 0; t < cnt; ++t) {
-            const int32_t k = kk[(int64_t)o * ksize + t];
-            sum += k;
-            int8_t b[3];
-            balanced_bytes(k, b);
-            const int pos = off + t, j = pos >> 2, bb = pos & 3;
-            int32_t* pl = grp(j);
-            for (int p = 0; p < 3; ++p) pl[p] |= (int32_t)((uint32_t)(uint8_t)b[p] << (8 * bb));
-        }
-        hdr[4 * o] = g0;
-        hdr[4 * o + 1] = ng;
-        hdr[4 * o + 2] = (int32_t)((1 << 21) + 128 * sum);
-        hdr[4 * o + 3] = 0;
-    }
-    return IPP_OK;
-}
 
 // ---------------------------------------------------------------------------
 // MFMA tile format (fused pipe, v_mfma_i32_16x16x64_i8).  Outputs are grouped
@@ -275,7 +215,7 @@ extern "C" int ipp_plan_dot4_from_taps(int32_t out_size, int32_t ksize, const in
 //           the B operand B[k][col] of the H pass and, unchanged, the A
 //           operand A[row][k] of the V pass (same lane map).
 // so that with pixels stored XOR 0x80 the i8 MFMA accumulators give
-//   2^21 + Σ p·k = bias + Σ_p 2^(8p) acc_p   exactly (as the dot4 format).
+//   2^21 + Σ p·k = bias + Σ_p 2^(8p) acc_p   exactly.
 // Layout per axis (int32 units): hdr[4T], bias[16T], blocks (4 int32 each).
 // ---------------------------------------------------------------------------
 namespace {
@@ -407,12 +347,14 @@ extern "C" int ipp_plan_mfma_tile(const ipp_tap_axis* a, int32_t t, int32_t hdr[
     return IPP_OK;
 }
 
-// Plan every axis of a pipe batch in the dot4 format.  Axis i resamples
+// Plan every axis of a pipe batch in the MFMA tile format.  Axis i resamples
 // in_sizes[i] → out_sizes[i]; identity[i] != 0 encodes "no pass on this axis"
 // (single 2^22 tap).  For axes with shift_first[i] != 0 the Pillow bounds are
 // shifted by their first xmin (ybox_first).  first_last[2i..2i+1] receives
-// (ybox_first, ybox_last) of the unshifted bounds.  offsets[i] = int32 offset
-// of the axis block in `out`, sized by ipp_plan_dot4_size(out, ksize(i)).
+// (ybox_first, ybox_last) of the unshifted bounds.  format[i] = 2 + phase
+// (IPP_TAPS_MFMA tiles, tile phase 0..15; any other value: IPP_E_ARG);
+// offsets[i] = int32 offset of the axis block in `out`, sized by
+// ipp_plan_mfma_size.
 extern "C" int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int32_t* out_sizes,
                                   const int32_t* identity, const int32_t* shift_first, const int32_t* transposed,
                                   const int64_t* offsets, int32_t* out, int32_t* first_last, int32_t n_threads) {
@@ -448,8 +390,7 @@ extern "C" int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int3
             const int e = transposed[i] >= 2
                               ? ipp_plan_mfma_from_taps(in, o, ksize, tmp.data(), shift_first[i] ? first : 0,
                                                         transposed[i] - 2, out + offsets[i])
-                              : ipp_plan_dot4_from_taps(o, ksize, tmp.data(), shift_first[i] ? first : 0,
-                                                        transposed[i], out + offsets[i]);
+                              : IPP_E_ARG;
             if (e) err[t] = e;
         }
     };

@@ -86,6 +86,28 @@ __device__ __forceinline__ void pair_regroup(uint32_t (&a)[4], bool o1) {
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
+// Cache policy of the H pass's tap loads and of the background copy's loads
+// (experiment switches; 0 = plain loads, 16 = sc1: served by L2, not kept in
+// the CU's L1, which the gathers need).
+#ifndef IPP_TAP_POL
+#define IPP_TAP_POL 0
+#endif
+#ifndef IPP_COPY_POL
+#define IPP_COPY_POL 0
+#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+template <int POL>
+__device__ __forceinline__ uint4 ld16_pol(const uint4* base, __amdgpu_buffer_rsrc_t rs, int idx) {
+#if defined(IPP_DIAG) && defined(IPP_DIAG_NOTAPS)
+    // diagnostic (wrong output): no tap loads, constant operands
+    { const uint32_t v = (uint32_t)idx * 0x01010101u; asm volatile("" :: "v"(v)); return make_uint4(v, v ^ 1u, v ^ 2u, v ^ 3u); }
+#endif
+    if (POL == 0) return base[idx];
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)idx * 16u, 0, POL));
+}
+
 // ---------------------------------------------------------------------------
 // H pass (MFMA taps): per-pixel buffer-load gathers, table-driven HSV test.
 //
@@ -266,6 +288,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
     const int32_t* tbias = coefs + h.coef_off + 4 * (int64_t)ntiles;
     const uint4* tblk = reinterpret_cast<const uint4*>(coefs + h.coef_off + 20 * (int64_t)ntiles);
+    const __amdgpu_buffer_rsrc_t brs = rsrc_of(tblk);
     const uint32_t sx = (uint32_t)HP_STEPC * (uint32_t)B.b0, sy = (uint32_t)HP_STEPC * (uint32_t)B.b3;  // per-step advance
 
     int filled = hdr[0].x;  // ring holds M columns [.., filled)
@@ -303,15 +326,13 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         int4 th = make_int4(0, 0, 0, 0);
         uint4 bn[3];
         int32_t bias = 0;  // the lane's output column bias, in flight with the taps
-        const uint4* bt = tblk + lane;
         {
             // Loaded unconditionally (a valid tile stands in when the wave
             // has none), so the loads in flight do not depend on the path.
             const int te = min(t, ntiles - 1);
             th = hdr[te];
-            bt += th.z;
 #pragma unroll
-            for (int p = 0; p < 3; ++p) bn[p] = bt[p * 64];
+            for (int p = 0; p < 3; ++p) bn[p] = ld16_pol<IPP_TAP_POL>(tblk, brs, th.z + lane + p * 64);
             const int xb = 16 * te + (lane & 15);
             bias = tbias[min(xb, h.out_len - 1)];
             if (!has_tile) th.y = 0;
@@ -425,7 +446,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                 for (int p = 0; p < 3; ++p) bq[p] = __builtin_bit_cast(i32x4, bn[p]);
                 if (ks + 1 < th.y) {
 #pragma unroll
-                    for (int p = 0; p < 3; ++p) bn[p] = bt[((ks + 1) * 3 + p) * 64];
+                    for (int p = 0; p < 3; ++p) bn[p] = ld16_pol<IPP_TAP_POL>(tblk, brs, th.z + lane + ((ks + 1) * 3 + p) * 64);
                 }
                 const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
 #pragma unroll
@@ -504,12 +525,17 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4* s4 = reinterpret_cast<const u32x4*>(sb);
         u32x4* d4 = reinterpret_cast<u32x4*>(db);
+        const __amdgpu_buffer_rsrc_t srs = rsrc_of(sb);
         for (int64_t i0 = a + threadIdx.x; i0 < e; i0 += U * NT) {
             u32x4 v[U];
 #pragma unroll
             for (int j = 0; j < U; ++j) {
                 const int64_t i = i0 + NT * j;
-                if (i < e) v[j] = s4[i < n0 ? i : i + skip];
+                if (i < e) {
+                    const int64_t k = i < n0 ? i : i + skip;
+                    if (IPP_COPY_POL == 0) v[j] = s4[k];
+                    else v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, (uint32_t)k * 16u, 0, IPP_COPY_POL));
+                }
             }
 #pragma unroll
             for (int j = 0; j < U; ++j) {

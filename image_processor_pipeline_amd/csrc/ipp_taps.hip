@@ -232,26 +232,38 @@ extern "C" int ipp_pipe_plan_taps(const ipp_tap_axis* axes, int32_t n_axes, int3
     if (ctl[0] > TAP_FLAG_CAP) return IPP_E_RANGE;
     if (ctl[0] == 0) return IPP_OK;
     std::vector<int2> fl(ctl[0]);
-    if (hipMemcpy(fl.data(), d_flags, fl.size() * sizeof(int2), hipMemcpyDeviceToHost) != hipSuccess)
+    // on `s`, not the null stream (which would wait for unrelated work, e.g.
+    // the batch running on another stream while this one is planned)
+    if (hipMemcpyAsync(fl.data(), d_flags, fl.size() * sizeof(int2), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
         return IPP_E_LAUNCH;
     // Rebuild the flagged tiles on the host (libm sin) and copy them over.
     int maxnk = 1;
     for (const int2& f : fl) maxnk = std::max(maxnk, axes[f.x].nkb);
     std::vector<int32_t> bias(16 * fl.size());
     std::vector<uint8_t> blocks((size_t)maxnk * 3072 * fl.size());
+    // Every tile is rebuilt before any copy is queued, and the copies (which
+    // read `bias` / `blocks`) have completed before this function returns on
+    // every path.
+    std::vector<int32_t> hdrs(4 * fl.size());
     for (size_t i = 0; i < fl.size(); ++i) {
+        const int e = ipp_plan_mfma_tile(&axes[fl[i].x], fl[i].y, hdrs.data() + 4 * i, bias.data() + 16 * i,
+                                         blocks.data() + i * (size_t)maxnk * 3072, (int64_t)maxnk * 3072);
+        if (e) return e;
+    }
+    int rc = IPP_OK;
+    for (size_t i = 0; i < fl.size() && rc == IPP_OK; ++i) {
         const ipp_tap_axis& a = axes[fl[i].x];
         const int t = fl[i].y;
-        int32_t hdr[4];
-        uint8_t* b = blocks.data() + i * (size_t)maxnk * 3072;
-        const int e = ipp_plan_mfma_tile(&a, t, hdr, bias.data() + 16 * i, b, (int64_t)maxnk * 3072);
-        if (e) return e;
+        const int32_t* hdr = hdrs.data() + 4 * i;
         int32_t* base = coefs + a.coef_off;
         if (hipMemcpyAsync(base + 4 * (int64_t)a.n_tiles + 16 * t, bias.data() + 16 * i, 64, hipMemcpyHostToDevice,
                            s) != hipSuccess ||
-            hipMemcpyAsync(base + 20 * (int64_t)a.n_tiles + 4 * (int64_t)hdr[2], b, (size_t)hdr[1] * 3072,
-                           hipMemcpyHostToDevice, s) != hipSuccess)
-            return IPP_E_LAUNCH;
+            hipMemcpyAsync(base + 20 * (int64_t)a.n_tiles + 4 * (int64_t)hdr[2],
+                           blocks.data() + i * (size_t)maxnk * 3072, (size_t)hdr[1] * 3072, hipMemcpyHostToDevice,
+                           s) != hipSuccess)
+            rc = IPP_E_LAUNCH;
     }
-    return hipStreamSynchronize(s) == hipSuccess ? IPP_OK : IPP_E_LAUNCH;
+    if (hipStreamSynchronize(s) != hipSuccess) return IPP_E_LAUNCH;
+    return rc;
 }

@@ -144,7 +144,9 @@ def fit_crop(image_path: Path, output_dirs: List[Path], **options: Any) -> Optio
             new_image = Image.fromarray(out, image.mode)
         if image.mode == "P":
             new_image.putpalette(image.getpalette())
-            new_image.info = dict(image.info)
+        # Image.crop keeps info for every mode (Image._new): icc_profile,
+        # transparency, dpi… reach the PNG writer as in the reference
+        new_image.info = dict(image.info)
     output_path = output_dir / image_path.name
     new_image.save(output_path)
     return output_path

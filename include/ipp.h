@@ -204,10 +204,9 @@ typedef struct ipp_pipe_desc {
     ipp_paste_desc p;       /* paste: ov = V-pass result (never stored)        */
 } ipp_pipe_desc;
 
-/* Tap formats (ipp_plan_pipe_axes transposed = 0/1 / 2 + phase).  The pipe
- * kernels take IPP_TAPS_MFMA only; any other value returns IPP_E_ARG.  The
- * dot4 format stays a host planning format (ipp_plan_dot4_*). */
-#define IPP_TAPS_DOT4 0   /* per-output dot4 planes (host planner only)       */
+/* Tap format of the pipe kernels (ipp_plan_pipe_axes format = 2 + phase).
+ * The pipe kernels take IPP_TAPS_MFMA only; any other value returns
+ * IPP_E_ARG. */
 #define IPP_TAPS_MFMA 1   /* 16-output tiles, v_mfma_i32_16x16x64_i8          */
 
 /* src_cn: channels of every source in the batch (3 or 4); hsv: HOST pointer.
@@ -340,17 +339,10 @@ int64_t ipp_plan_lanczos(int32_t in_size, double in0, double in1, int32_t out_si
 int ipp_plan_lanczos_batch(int32_t n, const int32_t* in_sizes, const int32_t* out_sizes,
                            const int64_t* offsets, int32_t* out, int64_t out_capacity,
                            int32_t n_threads);
-/* dot4 tap format of the fused pipe kernels (see ipp_host.cpp): per output
- * hdr (g0, ng, bias, 0) then ng tap groups of 3 balanced signed byte planes;
- * stride = groups reserved per output; size = int32 count for an axis. */
-int32_t ipp_plan_dot4_stride(int32_t ksize);
-int64_t ipp_plan_dot4_size(int32_t out_size, int32_t ksize);
-int ipp_plan_dot4_from_taps(int32_t out_size, int32_t ksize, const int32_t* std_taps,
-                            int32_t shift, int32_t transposed, int32_t* out);
-/* Plan every axis of a pipe batch in the dot4 format (threaded); identity[i]
- * = no pass on that axis; shift_first[i] = shift bounds to ybox_first;
- * transposed[i] = planes stored [group][output] (H pass) instead of
- * [output][group] (V pass); first_last receives (ybox_first, ybox_last). */
+/* Plan every axis of a pipe batch in the MFMA tile format (threaded);
+ * identity[i] = no pass on that axis; shift_first[i] = shift bounds to
+ * ybox_first; transposed[i] = 2 + tile phase (other values: IPP_E_ARG);
+ * first_last receives (ybox_first, ybox_last). */
 int ipp_plan_pipe_axes(int32_t n, const int32_t* in_sizes, const int32_t* out_sizes,
                        const int32_t* identity, const int32_t* shift_first,
                        const int32_t* transposed, const int64_t* offsets, int32_t* out,

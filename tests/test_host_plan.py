@@ -22,45 +22,6 @@ def test_lanczos_taps_match_oracle(io):
     assert np.array_equal(buf[2 * o:].reshape(o, k), taps)
 
 
-def _sdot4(a, b):
-    av = np.array([a], np.uint32).view(np.int8).astype(np.int64)
-    bv = np.array([b], np.uint32).view(np.int8).astype(np.int64)
-    return int((av * bv).sum())
-
-
-@pytest.mark.parametrize("io,shift", [((1100, 230), 0), ((1268, 307), 5), ((40, 40), 0), ((13, 40), 0)])
-def test_dot4_format_is_exact(io, shift):
-    """bias + Σ_b 2^(8b) Σ_j sdot4(p^0x80, plane_b) == 2^21 + Σ p·k for every
-    output, for random pixels (the identity the pipe kernels rely on)."""
-    lib = N.load()
-    i, o = io
-    k, std = G.lanczos_taps(i, o)
-    if shift:
-        std[0:2 * o:2] += shift   # pretend the axis starts `shift` rows later
-    ngs = lib.ipp_plan_dot4_stride(k)
-    out = np.zeros(lib.ipp_plan_dot4_size(o, k), np.int32)
-    assert lib.ipp_plan_dot4_from_taps(o, k, N.np_ptr(std), shift, 0, N.np_ptr(out)) == 0
-    outT = np.zeros_like(out)
-    assert lib.ipp_plan_dot4_from_taps(o, k, N.np_ptr(std), shift, 1, N.np_ptr(outT)) == 0
-    assert np.array_equal(outT[4 * o:].reshape(ngs, o, 4).transpose(1, 0, 2), out[4 * o:].reshape(o, ngs, 4))
-    hdr = out[:4 * o].reshape(o, 4)
-    planes = out[4 * o:].reshape(o, ngs, 4).view(np.uint32)
-    rng = np.random.default_rng(0)
-    pix = rng.integers(0, 256, i + 4 * ngs + 8, np.uint8)
-    for x in range(o):
-        xmin, cnt = std[2 * x] - shift, std[2 * x + 1]
-        ref = (1 << 21) + int((pix[xmin:xmin + cnt].astype(np.int64) * std[2 * o + x * k: 2 * o + x * k + cnt]).sum())
-        g0, ng, bias = hdr[x, 0], hdr[x, 1], hdr[x, 2]
-        assert g0 % 4 == 0 and g0 <= xmin and ng <= ngs
-        acc = [0, 0, 0]
-        for j in range(ngs):
-            w = (pix[g0 + 4 * j: g0 + 4 * j + 4] ^ 0x80).view(np.uint32)[0]
-            for b in range(3):
-                acc[b] += _sdot4(int(w), int(planes[x, j, b]))
-        got = bias + acc[0] + (acc[1] << 8) + (acc[2] << 16)
-        assert got == ref, x
-
-
 @pytest.mark.parametrize("wh", [(896, 896), (53, 37), (2, 3), (1, 9), (640, 480)])
 def test_opaque_bbox_matches_bruteforce(wh):
     w, h = wh

@@ -15,7 +15,7 @@ for name in "$@"; do
              "TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_ADDR_STALL_CYCLES_sum TCP_TCC_READ_REQ_LATENCY_sum" \
              "TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_ADDR_STALLED_BY_TD_CYCLES_sum SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_SALU"; do
     i=$((i+1))
-    timeout -s KILL 120 rocprofv3 --kernel-include-regex "$FILTER" --pmc $grp --output-format csv -d $OUT/p$i -o p$i -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-copy-ceiling > $OUT/p$i.log 2>&1 || { tail -5 $OUT/p$i.log; exit 31; }
+    timeout -s KILL 120 rocprofv3 --kernel-include-regex "$FILTER" --pmc $grp --output-format csv -d $OUT/p$i -o p$i -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-copy-ceiling --no-stream > $OUT/p$i.log 2>&1 || { tail -5 $OUT/p$i.log; exit 31; }
   done
   python tools/prof_summary.py $OUT > $OUT/summary.txt 2>&1 || true
   find $OUT -name '*counter_collection.csv' -size +4M -delete

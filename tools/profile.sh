@@ -7,7 +7,7 @@
 # Usage: tools/profile.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-prof}; shift
-ARGS=${@:---steps 3 --warmup 1 --no-cpu-baseline}
+ARGS=${@:---steps 3 --warmup 1 --no-cpu-baseline --no-stream}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
