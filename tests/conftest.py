@@ -80,3 +80,65 @@ def config3_black_source(i: int) -> np.ndarray:
     src[500 + 11 * i:503 + 11 * i, :] = 0
     src[r.random((1024, 1024)) < 0.03] = 0
     return src
+
+# V / S-only exclusion ranges (pipe_config3_vs_pillow.npz): every range is
+# fixed by V = max(r, g, b) alone or by S = 0 (r = g = b: diff 0 gives s = 0
+# in any HSV conversion, and diff ≥ 1 gives s ≥ 1 with OpenCV's tables), with
+# H and the other channel unconstrained, so the exclusion mask is exact
+# without OpenCV.  Zones restrict two of them to windows of the cut-out M.
+VS_RANGES = [(0, 0, 0, 180, 255, 40),       # dark (fill included)
+             (0, 0, 96, 180, 255, 112),     # a band of V
+             (0, 0, 0, 180, 0, 255)]        # grey (S = 0)
+VS_ZONES = [None, (150, 40, 90, 260), (60, 200, 0, 120)]
+CONFIG3_VS_SEED = 6000
+
+
+def config3_vs_source(i: int) -> np.ndarray:
+    """Item i's 1024² source for pipe_config3_vs_pillow.npz: a structured
+    scene — colour gradients, exact greys (S = 0) at several levels (some dark,
+    some inside the V band), near-greys (r = g = b + 1, S > 0), dark and
+    V-band coloured shapes, thin grey lines and a noise patch — so the cut-out
+    gets α edges from every range, their OR and the zone borders."""
+    r = np.random.default_rng(CONFIG3_VS_SEED + i)
+    yy, xx = np.mgrid[0:1024, 0:1024].astype(np.float64)
+    src = np.empty((1024, 1024, 3), np.uint8)
+    src[..., 0] = (xx / 4 + 30 * i) % 256
+    src[..., 1] = (yy / 4 + 50 * np.sin(xx / 97.0 + i)) % 256
+    src[..., 2] = 128 + 100 * np.sin((xx + yy) / 151.0 + 0.7 * i)
+    for _ in range(14):
+        y0, x0 = (int(v) for v in r.integers(0, 960, 2))
+        hh, ww = (int(v) for v in r.integers(20, 240, 2))
+        kind = int(r.integers(0, 5))
+        lvl = int(r.choice([20, 38, 100, 104, 111, 150, 200, 255]))
+        if kind == 0:                                    # exact grey rectangle
+            src[y0:y0 + hh, x0:x0 + ww] = lvl
+        elif kind == 1:                                  # near grey (S > 0)
+            src[y0:y0 + hh, x0:x0 + ww] = (lvl, lvl, max(lvl - 1, 0))
+        elif kind == 2:                                  # grey disc
+            m = (yy - y0) ** 2 + (xx - x0) ** 2 < (hh / 2) ** 2
+            src[m] = lvl
+        elif kind == 3:                                  # coloured shape of V = lvl
+            src[y0:y0 + hh, x0:x0 + ww] = (lvl, lvl // 3, (2 * lvl) // 5)
+        else:                                            # noise patch
+            src[y0:y0 + hh, x0:x0 + ww] = r.integers(0, 256, src[y0:y0 + hh, x0:x0 + ww].shape)
+    for k in range(6):                                   # thin grey lines, 1-3 px
+        c = 180 + 90 * k + 13 * i
+        src[:, c:c + 1 + k % 3] = 60 + 30 * k
+        src[c:c + 1 + (k + 1) % 3, :] = 104 if k % 2 else 255
+    return src
+
+
+def vs_alpha(rgb: np.ndarray) -> np.ndarray:
+    """filtres_liste.py:97-134 α for VS_RANGES / VS_ZONES on the cut-out's RGB
+    (any channel order): 0 where some range holds inside its zone."""
+    h, w = rgb.shape[:2]
+    v = rgb.max(axis=2).astype(np.int32)
+    grey = rgb.min(axis=2).astype(np.int32) == v
+    holds = [v <= 40, (v >= 96) & (v <= 112), grey]
+    excl = np.zeros((h, w), bool)
+    for hold, zone in zip(holds, VS_ZONES):
+        zt, zb, zl, zr = zone if zone else (0, 0, 0, 0)
+        zm = np.zeros((h, w), bool)
+        zm[zt:h - zb, zl:w - zr] = True      # numpy slice, as zone_mask[...] = 255
+        excl |= hold & zm
+    return np.where(excl, 0, 255).astype(np.uint8)

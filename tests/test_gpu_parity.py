@@ -668,3 +668,30 @@ def test_pipe_config3_geometry_matches_pillow(D, golden, i):
     out = torch.empty((1, 1024, 1024, 3), dtype=torch.uint8, device=DEV)
     runner.run(_t(src[None]), _t(bgs), out)
     assert sha256(out[0].cpu().numpy()) == str(g["comp_sha"][i])
+
+
+@pytest.mark.parametrize("i", range(6))
+def test_pipe_config3_vs_ranges_match_pillow(D, golden, i):
+    """The pipe's HSV stage with several ranges OR-ed and zone masks, at
+    config-3 geometry on a structured scene (pipe_config3_vs_pillow.npz): the
+    ranges are fixed by V or by S = 0 alone, so the exclusion mask — and the
+    partial-α edges it leaves after the ≈5× LANCZOS downscale — is exact
+    without OpenCV, and the composite is Pillow's."""
+    from image_processor_pipeline_amd import fused
+    from tests.conftest import VS_RANGES, VS_ZONES, config3_vs_source, sha256
+    g = golden("pipe_config3_vs_pillow.npz")
+    src = config3_vs_source(i)
+    bgs = np.stack([np.random.default_rng(int(g["bg_seed"]) + k).integers(0, 256, (1024, 1024, 3), np.uint8)
+                    for k in range(2)])
+    x, y = (int(v) for v in g["xy"][i])
+    cfg = fused.PipeConfig(hsv_ranges=list(VS_RANGES), zones=list(VS_ZONES))
+    plan = fused.plan_pipe((1024, 1024), 1, (1024, 1024), 2, cfg,
+                           params=[fused.ItemParams(float(g["angles"][i]), str(g["syms"][i]), int(g["bg_index"][i]),
+                                                    float(g["ratios"][i]), x, y)])
+    assert plan.ov_dims[0] == tuple(int(v) for v in g["ov_wh"][i])[::-1]
+    runner = fused.PipeRunner(plan, DEV)
+    out = torch.empty((1, 1024, 1024, 3), dtype=torch.uint8, device=DEV)
+    runner.run(_t(src[None]), _t(bgs), out)
+    assert runner.status() == 0
+    assert sha256(out[0].cpu().numpy()) == str(g["comp_sha"][i])
+
