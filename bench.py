@@ -61,11 +61,6 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=192)
     ap.add_argument("--no-copy-ceiling", action="store_true")
-    ap.add_argument("--unsplit", action="store_true", help="pipe5: ipp_pipe_hpass + full-frame ipp_pipe_vblend")
-    ap.add_argument("--fused", action="store_true",
-                    help="pipe5: the one-launch ipp_pipe_fused instead of ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands "
-                         "(the two-launch split form, the default: measured 1-2 %% faster on MI355X, DESIGN.md §3)")
-    ap.add_argument("--split", action="store_true", help="pipe5: the split form (the default; kept for scripts)")
     ap.add_argument("--stream", action="store_true",
                     help="pipe5: the streaming leg (the default; kept for scripts)")
     ap.add_argument("--no-stream", action="store_true",
@@ -309,20 +304,11 @@ def main(argv=None):
             runner = fused.PipeRunner(plan, dev)
             setup["taps_device_ms"] = round((time.perf_counter() - t_host) * 1e3, 1)
             setup["taps_host_tiles"] = runner.host_tiles
-            if runner.split and not args.unsplit and args.fused:
-                # one launch: H pass, background copy, V pass + paste (ipp_pipe_fused)
-                algo = {"ipp_pipe_fused": plan.algo_bytes_hpass_bgcopy + plan.algo_bytes_vblend_bands}
-                launches = [("ipp_pipe_fused", lambda: runner.fused(src, bgs, out))]
-            elif runner.split and not args.unsplit:
-                # the H pass also copies the background rows outside the overlay bands
-                algo = {"ipp_pipe_hpass_bgcopy": plan.algo_bytes_hpass_bgcopy,
-                        "ipp_pipe_vblend_bands": plan.algo_bytes_vblend_bands}
-                launches = [("ipp_pipe_hpass_bgcopy", lambda: runner.hpass_bgcopy(src, bgs, out)),
-                            ("ipp_pipe_vblend_bands", lambda: runner.vblend_bands(bgs, out))]
-            else:
-                algo = {"ipp_pipe_hpass": plan.algo_bytes_hpass, "ipp_pipe_vblend": plan.algo_bytes_vblend}
-                launches = [("ipp_pipe_hpass", lambda: runner.hpass(src)),
-                            ("ipp_pipe_vblend", lambda: runner.vblend(bgs, out))]
+            # the H pass also copies the background rows outside the overlay bands
+            algo = {"ipp_pipe_hpass_bgcopy": plan.algo_bytes_hpass_bgcopy,
+                    "ipp_pipe_vblend_bands": plan.algo_bytes_vblend_bands}
+            launches = [("ipp_pipe_hpass_bgcopy", lambda: runner.hpass_bgcopy(src, bgs, out)),
+                        ("ipp_pipe_vblend_bands", lambda: runner.vblend_bands(bgs, out))]
         outputs = lambda: {start + i: _digest(out[i].cpu().numpy()) for i in range(B)}
         workload = "5-stage pipe: crop(64px)->rotate(NEAREST,expand,bbox)->flip->HSV mask(4 ref ranges)->LANCZOS+paste"
     elif args.workload == "video4k":

@@ -125,12 +125,8 @@ SIGNATURES = {
     "ipp_lanczos_h": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ipp_lanczos_v": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "ipp_paste_blend": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
-    "ipp_pipe_hpass": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P]),
-    "ipp_pipe_vblend": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "ipp_pipe_hpass_bgcopy": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _P]),
     "ipp_pipe_vblend_bands": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
-    "ipp_pipe_sync_bytes": (_L, [_I, _I, _I]),
-    "ipp_pipe_fused": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P]),
     "ipp_ccl_keep_largest": (_I, [_P, _P, _I, _I, _I, _P, _P, _L, _P, _P, _P, _P]),
     "ipp_ccl_scratch_layout": (_L, [_I, _I, _P]),
     "ipp_video_keep_largest": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _L, _P, _P, _P, _P, _P, _P]),

@@ -23,6 +23,7 @@
 // rows] bytes (16 B per (g, x')), values XOR 0x80.  T rows are M rows
 // [line0, line0 + lines).
 #include <algorithm>
+#include <type_traits>
 
 #include "ipp_hsv.h"
 #include "ipp_sampler.h"
@@ -94,6 +95,10 @@ typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 #endif
 #ifndef IPP_COPY_POL
 #define IPP_COPY_POL 0
+#endif
+// Tap loads masked to the lanes whose 16 taps can be nonzero (experiment switch).
+#ifndef IPP_TAP_MASK
+#define IPP_TAP_MASK 0
 #endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFFF, 0x00020000);
@@ -276,7 +281,7 @@ __device__ __forceinline__ Hp2Chunk hp2_chunk(const int4* hdr, int s0, int ntile
     return c;
 }
 
-template <int NR, bool ZONES, int CN, bool CLAMP, bool SC1>
+template <int NR, bool ZONES, int CN, bool CLAMP>
 __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win, int wave, const Hp2Block& B,
                                             uint8_t* __restrict__ tmp,
                                             const int32_t* __restrict__ coefs, const ipp_resample_desc& h,
@@ -289,6 +294,10 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     const int32_t* tbias = coefs + h.coef_off + 4 * (int64_t)ntiles;
     const uint4* tblk = reinterpret_cast<const uint4*>(coefs + h.coef_off + 20 * (int64_t)ntiles);
     const __amdgpu_buffer_rsrc_t brs = rsrc_of(tblk);
+    // Pillow's LANCZOS support in M columns (Resample.c precompute_coeffs:
+    // center (o + 0.5)·scale, support 3·max(scale, 1)), for the tap lane masks
+    const float scale = (float)h.in_len / (float)h.out_len;
+    const float support = 3.0f * fmaxf(scale, 1.0f);
     const uint32_t sx = (uint32_t)HP_STEPC * (uint32_t)B.b0, sy = (uint32_t)HP_STEPC * (uint32_t)B.b3;  // per-step advance
 
     int filled = hdr[0].x;  // ring holds M columns [.., filled)
@@ -325,14 +334,28 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         const bool has_tile = t < ck.s1 && nrows > 0;
         int4 th = make_int4(0, 0, 0, 0);
         uint4 bn[3];
+        float tap_lo, tap_hi;  // the lane's K-step starts with nonzero taps lie in (tap_lo, tap_hi)
         int32_t bias = 0;  // the lane's output column bias, in flight with the taps
         {
             // Loaded unconditionally (a valid tile stands in when the wave
             // has none), so the loads in flight do not depend on the path.
             const int te = min(t, ntiles - 1);
             th = hdr[te];
+            // The lane's 16 taps of a K step are zero outside its output's
+            // support; those lanes load nothing (masked) and take zeros.
+            tap_lo = -1e30f;
+            tap_hi = 1e30f;
+            if (IPP_TAP_MASK) {
+                const float c = ((float)(16 * te + (lane & 15)) + 0.5f) * scale;
+                tap_lo = c - support - 2.0f - (float)(16 * (lane >> 4) + 16);
+                tap_hi = c + support + 2.0f - (float)(16 * (lane >> 4));
+            }
+            const bool act0 = (float)th.x < tap_hi && (float)th.x > tap_lo;
 #pragma unroll
-            for (int p = 0; p < 3; ++p) bn[p] = ld16_pol<IPP_TAP_POL>(tblk, brs, th.z + lane + p * 64);
+            for (int p = 0; p < 3; ++p) {
+                bn[p] = make_uint4(0u, 0u, 0u, 0u);
+                if (act0) bn[p] = ld16_pol<IPP_TAP_POL>(tblk, brs, th.z + lane + p * 64);
+            }
             const int xb = 16 * te + (lane & 15);
             bias = tbias[min(xb, h.out_len - 1)];
             if (!has_tile) th.y = 0;
@@ -445,8 +468,13 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
 #pragma unroll
                 for (int p = 0; p < 3; ++p) bq[p] = __builtin_bit_cast(i32x4, bn[p]);
                 if (ks + 1 < th.y) {
+                    const float kg = (float)(th.x + 64 * (ks + 1));
+                    const bool act = kg < tap_hi && kg > tap_lo;
 #pragma unroll
-                    for (int p = 0; p < 3; ++p) bn[p] = ld16_pol<IPP_TAP_POL>(tblk, brs, th.z + lane + ((ks + 1) * 3 + p) * 64);
+                    for (int p = 0; p < 3; ++p) {
+                        bn[p] = make_uint4(0u, 0u, 0u, 0u);
+                        if (act) bn[p] = ld16_pol<IPP_TAP_POL>(tblk, brs, th.z + lane + ((ks + 1) * 3 + p) * 64);
+                    }
                 }
                 const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
 #pragma unroll
@@ -471,12 +499,10 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                 uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
                 const uint32_t w[4] = {outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
                                        outc[3] ^ 0x80808080u};
-                // SC1 (fused launch): written through to memory, for the V
-                // blocks of another CU / XCD that read it in the same launch.
-                // Else nontemporal: T is read back only after the whole launch
+                // Nontemporal: T is read back only after the whole launch
                 // (-0.8 % against plain stores; nontemporal T loads in the V
                 // pass measured +15 %).
-                store16<SC1 ? 1 : 2>(reinterpret_cast<uint8_t*>(dst), 16, true, w);
+                store16<2>(reinterpret_cast<uint8_t*>(dst), 16, true, w);
             }
         }
         // The next chunk's first sets are waited for here, at the end of
@@ -563,15 +589,12 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
     }
 }
 
-// One H-pass block: band tb of item im.  SYNC (fused launch): T is stored
-// write-through and, once every wave's stores have drained, the block adds one
-// to the item's completion counter (agent scope) — the hand-off protocol of
-// MI355X_MICROARCH.md §Correctness boundaries for a consumer on any CU / XCD.
-template <int NR, bool ZONES, int CN, bool SYNC>
+// One H-pass block: band tb of item im.
+template <int NR, bool ZONES, int CN>
 __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __restrict__ src,
                                             uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
                                             const ipp_pipe_desc* __restrict__ descs, int im, int tb,
-                                            const ipp_hsv_params& hp, int32_t* __restrict__ done) {
+                                            const ipp_hsv_params& hp) {
     const ipp_gather_desc g = descs[im].g;
     const ipp_resample_desc h = descs[im].h;
     const int row0 = tb * HR;
@@ -659,39 +682,34 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
     const uint32_t fill = hsv2_px<NR, ZONES>(L.T, 0u, ~0u);
     const int nrows = min(HR, h.lines - row0);
     if (CN == 3 && clamp)
-        hpass2_body<NR, ZONES, CN, true, SYNC>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+        hpass2_body<NR, ZONES, CN, true>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
     else
-        hpass2_body<NR, ZONES, CN, false, SYNC>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
-    if (SYNC) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's T stores have reached memory
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_fetch_add(done + im, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+        hpass2_body<NR, ZONES, CN, false>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
 }
 
 // 4 waves per SIMD (≤ 128 VGPRs); the > 8-range zone forms get 3 (they spill
 // at 128, and nothing may spill between an asm gather and its wait).
-template <int NR, bool ZONES, int CN, bool COPY>
+template <int NR, bool ZONES, int CN>
 __global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES && NR > 8 ? 3 : 4)))
 k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
               const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp, const uint8_t* __restrict__ bg,
               uint8_t* __restrict__ dst, int cpi) {
     __shared__ Hpass2Lds<NR> L;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    // tiles_y = H-pass blocks per item.  COPY: each item owns tiles_y H-pass
+    // tiles_y = H-pass blocks per item.  Each item owns tiles_y H-pass
     // blocks followed by cpi background-copy blocks, so the copies run beside
     // the H pass on every XCD.
-    const int per_item = tiles_y + (COPY ? cpi : 0);
+    const int per_item = tiles_y + cpi;
     const int im = b / per_item;
     const int tb = b - im * per_item;
-    if (COPY && tb >= tiles_y) {
+    if (tb >= tiles_y) {
         bg_copy_outside_bands<64 * HP_NW>(descs[im].p, bg, dst, tb - tiles_y, cpi);
         return;
     }
 #if defined(IPP_DIAG) && defined(IPP_DIAG_COPY_ONLY)
     return;  // diagnostic (wrong output): the copy blocks alone
 #endif
-    hpass_block<NR, ZONES, CN, false>(L, src, tmp, coefs, descs, im, tb, hp, nullptr);
+    hpass_block<NR, ZONES, CN>(L, src, tmp, coefs, descs, im, tb, hp);
 }
 
 // V pass on MFMA (tap tiles aligned with 16-row background bands: the plan's
@@ -701,6 +719,10 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
 // step), B = 64 T rows × 16 overlay columns of one channel (four 16-B T groups
 // per lane give all four channels), D lane l = column l&15, rows 4(l>>4)..+3.
 constexpr int VBR = 16;
+// V pass: the band's taps loaded once for all its column tiles (nK ≤ 4).
+#ifndef IPP_VB_HOIST
+#define IPP_VB_HOIST 1
+#endif
 // Diagnostic builds only (-DIPP_DIAG -DIPP_VB_X=…, wrong output): bit 0 = no
 // blend, bit 1 = no unpremultiply, bit 2 = no background copy loop.
 #if defined(IPP_DIAG) && defined(IPP_VB_X)
@@ -754,16 +776,16 @@ __device__ __forceinline__ void blend48(uint32_t (&bg)[12], const uint32_t (&ov)
     }
 }
 
-// One V-pass block: 16-row band ty of item im (BANDS: counted from the first
-// overlay band).  SC1: T is read past the caches (the fused launch's hand-off).
-template <int STORE, int DBG, bool BANDS, bool SC1>
+// One V-pass block: band ty of item im, counted from the first 16-row band
+// the overlay touches (the rows outside those bands: ipp_pipe_hpass_bgcopy).
+template <int STORE, int DBG>
 __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const uint8_t* __restrict__ tmp,
                                              const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
                                              const int32_t* __restrict__ coefs,
                                              const ipp_pipe_desc* __restrict__ descs, int im, int ty, int ov_w_max) {
     const ipp_paste_desc p = descs[im].p;
     int y0 = ty * VBR;
-    if (BANDS) {  // only the 16-row bands the overlay touches (the rest: ipp_pipe_hpass_bgcopy)
+    {
         int vb0, vb1;
         paste_bands(p, vb0, vb1);
         y0 += vb0;
@@ -799,61 +821,89 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
         int32_t rb[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) rb[r] = tbias[16 * t + 4 * (lane >> 4) + r];
-        const uint64_t tbase = reinterpret_cast<uint64_t>(tmp + v.src_off);
-        const __amdgpu_buffer_rsrc_t trs =
-            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(tbase), (short)0, 0x7FFFFFFF, 0x00020000);
-        for (int ct = wave; ct < ctiles; ct += 4) {
-            const int x = 16 * ct + x_l;
-            const int xs = min(x, p.ov_w - 1);
-            i32x4 acc[4][3];
+        // The band's taps (the A operand) are the same for every column tile:
+        // with nK ≤ 4 they are loaded once, before the column tiles, and every
+        // tile's T groups for all its K steps are issued before its MFMAs.
+        auto tiles = [&](auto nkc) {
+            constexpr int NK = decltype(nkc)::value;
+            i32x4 ta[NK > 0 ? NK : 1][3];
+            if (NK > 0) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                acc[c][0] = i32x4{rb[0], rb[1], rb[2], rb[3]};
-                acc[c][1] = i32x4{0, 0, 0, 0};
-                acc[c][2] = i32x4{0, 0, 0, 0};
-            }
-#pragma unroll 1
-            for (int ks = 0; ks < th.y; ++ks) {
-                i32x4 a[3];
-#pragma unroll
-                for (int q = 0; q < 3; ++q) a[q] = __builtin_bit_cast(i32x4, tblk[th.z + (ks * 3 + q) * 64 + lane]);
-                const int G = (th.x + 64 * ks + 16 * (lane >> 4)) >> 2;
-                uint4 g[4];
-                if (SC1) {
-                    const uint32_t o0 = (uint32_t)(G * v.src_pitch + 16 * xs);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        g[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                             trs, o0 + (uint32_t)(j * v.src_pitch), 0, 16));
-                } else {
-                    const uint4* tq = reinterpret_cast<const uint4*>(tmp + v.src_off + (int64_t)G * v.src_pitch) + xs;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) g[j] = tq[j * gstride];
-                }
-                const i32x4 bq[4] = {i32x4{(int)g[0].x, (int)g[1].x, (int)g[2].x, (int)g[3].x},
-                                     i32x4{(int)g[0].y, (int)g[1].y, (int)g[2].y, (int)g[3].y},
-                                     i32x4{(int)g[0].z, (int)g[1].z, (int)g[2].z, (int)g[3].z},
-                                     i32x4{(int)g[0].w, (int)g[1].w, (int)g[2].w, (int)g[3].w}};
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
+                for (int ks = 0; ks < NK; ++ks)
 #pragma unroll
                     for (int q = 0; q < 3; ++q)
-                        acc[c][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[q], bq[c], acc[c][q], 0, 0, 0);
+                        ta[ks][q] = __builtin_bit_cast(i32x4, tblk[th.z + (ks * 3 + q) * 64 + lane]);
             }
-            if (x < p.ov_w) {
+            for (int ct = wave; ct < ctiles; ct += 4) {
+                const int x = 16 * ct + x_l;
+                const int xs = min(x, p.ov_w - 1);
+                i32x4 acc[4][3];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = 4 * (lane >> 4) + r;   // band row = tile row
-                    const int o = y0 + row - p.y;           // overlay row
-                    if (o >= oy_lo && o < oy_hi) {
-                        uint32_t px = 0;
+                for (int c = 0; c < 4; ++c) {
+                    acc[c][0] = i32x4{rb[0], rb[1], rb[2], rb[3]};
+                    acc[c][1] = i32x4{0, 0, 0, 0};
+                    acc[c][2] = i32x4{0, 0, 0, 0};
+                }
+                // T groups of K step ks: rows th.x + 64 ks + 16 (lane >> 4) .. + 15
+                const uint4* tq0 = reinterpret_cast<const uint4*>(tmp + v.src_off) + xs;
+                const int gbase = (th.x + 16 * (lane >> 4)) >> 2;
+#define IPP_VB_TLOAD(ks, g)                                                                  \
+    {                                                                                        \
+        const uint4* tq = tq0 + (int64_t)(gbase + 16 * (ks)) * gstride;                      \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j) (g)[j] = tq[j * gstride];              \
+    }
+#define IPP_VB_MFMA(a, g)                                                                    \
+    {                                                                                        \
+        const i32x4 bq[4] = {i32x4{(int)(g)[0].x, (int)(g)[1].x, (int)(g)[2].x, (int)(g)[3].x}, \
+                             i32x4{(int)(g)[0].y, (int)(g)[1].y, (int)(g)[2].y, (int)(g)[3].y}, \
+                             i32x4{(int)(g)[0].z, (int)(g)[1].z, (int)(g)[2].z, (int)(g)[3].z}, \
+                             i32x4{(int)(g)[0].w, (int)(g)[1].w, (int)(g)[2].w, (int)(g)[3].w}}; \
+        _Pragma("unroll") for (int c = 0; c < 4; ++c)                                        \
+            _Pragma("unroll") for (int q = 0; q < 3; ++q)                                    \
+                acc[c][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8((a)[q], bq[c], acc[c][q], 0, 0, 0); \
+    }
+                if (NK > 0) {
+                    uint4 g[NK > 0 ? NK : 1][4];
 #pragma unroll
-                        for (int c = 0; c < 4; ++c)
-                            px |= clip8(acc[c][0][r] + (acc[c][1][r] << 8) + (acc[c][2][r] << 16)) << (8 * c);
-                        orow[row * os + xo + x] = (kVbX & 2) ? px : unpremultiply(px);
+                    for (int ks = 0; ks < NK; ++ks) IPP_VB_TLOAD(ks, g[ks])
+#pragma unroll
+                    for (int ks = 0; ks < NK; ++ks) IPP_VB_MFMA(ta[ks], g[ks])
+                } else {
+#pragma unroll 1
+                    for (int ks = 0; ks < th.y; ++ks) {
+                        i32x4 a[3];
+#pragma unroll
+                        for (int q = 0; q < 3; ++q)
+                            a[q] = __builtin_bit_cast(i32x4, tblk[th.z + (ks * 3 + q) * 64 + lane]);
+                        uint4 g[4];
+                        IPP_VB_TLOAD(ks, g)
+                        IPP_VB_MFMA(a, g)
+                    }
+                }
+#undef IPP_VB_TLOAD
+#undef IPP_VB_MFMA
+                if (x < p.ov_w) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = 4 * (lane >> 4) + r;   // band row = tile row
+                        const int o = y0 + row - p.y;           // overlay row
+                        if (o >= oy_lo && o < oy_hi) {
+                            uint32_t px = 0;
+#pragma unroll
+                            for (int c = 0; c < 4; ++c)
+                                px |= clip8(acc[c][0][r] + (acc[c][1][r] << 8) + (acc[c][2][r] << 16)) << (8 * c);
+                            orow[row * os + xo + x] = (kVbX & 2) ? px : unpremultiply(px);
+                        }
                     }
                 }
             }
+        };
+        switch (IPP_VB_HOIST ? th.y : 0) {
+            case 1: tiles(std::integral_constant<int, 1>{}); break;
+            case 2: tiles(std::integral_constant<int, 2>{}); break;
+            case 3: tiles(std::integral_constant<int, 3>{}); break;
+            case 4: tiles(std::integral_constant<int, 4>{}); break;
+            default: tiles(std::integral_constant<int, 0>{}); break;
         }
         __syncthreads();
     }
@@ -940,7 +990,7 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
     }
 }
 
-template <int STORE, int DBG = 0, bool BANDS = false>
+template <int STORE, int DBG = 0>
 __global__ void __launch_bounds__(256)
 k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
                    const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int tiles_y,
@@ -949,256 +999,80 @@ k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ 
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int im = b / tiles_y;
     const int ty = b - im * tiles_y;
-    vblend_block<STORE, DBG, BANDS, false>(orow, tmp, bg, dst, coefs, descs, im, ty, ov_w_max);
+    vblend_block<STORE, DBG>(orow, tmp, bg, dst, coefs, descs, im, ty, ov_w_max);
 }
-
-// ---------------------------------------------------------------------------
-// Fused launch (ipp_pipe_fused): per item, its H-pass blocks, its background
-// copy blocks and — D items later in the block order — its V-pass bands, so
-// the latency-bound V pass runs beside the VALU-bound H pass.  A V block reads
-// the item's completion counter (agent scope) once: if every H block of the
-// item has finished it proceeds, reading T past the caches; otherwise it
-// queues its band and exits (no spinning: correctness does not depend on the
-// dispatch order or on the XCD a block lands on).  k_pipe_vdeferred then runs
-// the queued bands after the launch.
-//
-// Sync scratch (ipp_pipe_sync_bytes): int32 done[n]; int32 nq; int32 queue[n·tyv].
-// ---------------------------------------------------------------------------
-constexpr int FUSE_LAG = 4;  // items between an item's H blocks and its V bands
-
-// The fused launch's LDS: an H block's ring and tables, or a V band's
-// unpremultiplied overlay rows (VBR × orow_stride(ov_w_max) words, at most
-// the H pass's size: ov_w_max ≤ ≈ 550 px; wider overlays take the split form).
-template <int NR>
-struct FusedLds {
-    union {
-        Hpass2Lds<NR> h;
-        uint32_t orow[sizeof(Hpass2Lds<NR>) / 4];
-    };
-    int32_t ready;
-};
-
-// (5-6 zoned ranges: 3 waves per SIMD too — at 4 the 3-channel form spilled
-// one register, and nothing may spill in a kernel with hand-waited gathers.)
-template <int NR, bool ZONES, int CN>
-__global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES && NR > 4 ? 3 : 4)))
-k_pipe_fused(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
-             const ipp_pipe_desc* __restrict__ descs, int n, int tyb, int cpi, int tyv, ipp_hsv_params hp,
-             const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst, int ov_w_max, int32_t* __restrict__ sync) {
-    // Static LDS: the H pass's table addresses then fold into the ds_read
-    // offset fields (through a dynamic region the compiler added the region's
-    // base to every table address: three v_add per gathered pixel).  The V
-    // bands' overlay rows share the region (the host checks they fit).
-    __shared__ FusedLds<NR> F;
-    const uint32_t L = xcd_remap(blockIdx.x, gridDim.x);
-    const int A = tyb + cpi, U = A + tyv, D = min(FUSE_LAG, n);
-    // Block order: items 0..D-1 (H, copy); then per item i ≥ D: H(i), copy(i),
-    // V(i - D); then V(n - D .. n - 1).
-    int role, im, k;  // role 0: H / copy (k < tyb: H band k), 1: V band k
-    if (L < (uint32_t)(D * A)) {
-        role = 0;
-        im = L / A;
-        k = L - im * A;
-    } else if (L < (uint32_t)(D * A + (n - D) * U)) {
-        const int l = L - D * A;
-        const int q = l / U, r = l - q * U;
-        if (r < A) { role = 0; im = D + q; k = r; }
-        else { role = 1; im = q; k = r - A; }
-    } else {
-        const int l = L - D * A - (n - D) * U;
-        role = 1;
-        im = n - D + l / tyv;
-        k = l - (l / tyv) * tyv;
-    }
-    if (role == 0) {
-        if (k >= tyb) {
-            bg_copy_outside_bands<64 * HP_NW>(descs[im].p, bg, dst, k - tyb, cpi);
-            return;
-        }
-        hpass_block<NR, ZONES, CN, true>(F.h, src, tmp, coefs, descs, im, k, hp, sync);
-        return;
-    }
-    {
-        // V band k of item im: nothing to do past the overlay bands
-        int vb0, vb1;
-        paste_bands(descs[im].p, vb0, vb1);
-        if (vb0 + VBR * k >= vb1) return;
-    }
-    int32_t& ready = F.ready;
-    if (threadIdx.x == 0) {
-        const int need = (descs[im].h.lines + HR - 1) / HR;
-        const int got = __hip_atomic_load(sync + im, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ready = got >= need;
-        if (!ready) {
-            const int slot = __hip_atomic_fetch_add(sync + n, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(sync + n + 1 + slot, im * tyv + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    __syncthreads();
-    if (!ready) return;
-    vblend_block<2, 0, true, true>(F.orow, tmp, bg, dst, coefs, descs, im, k, ov_w_max);
-}
-
-// The bands queued by k_pipe_fused (after it: every H block has finished).
-__global__ void __launch_bounds__(256)
-k_pipe_vdeferred(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
-                 const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int n, int tyv,
-                 int ov_w_max, const int32_t* __restrict__ sync) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t orow[];
-    const int nq = sync[n];
-    for (int e = blockIdx.x; e < nq; e += gridDim.x) {
-        const int code = sync[n + 1 + e];
-        const int im = code / tyv, k = code - im * tyv;
-        vblend_block<2, 0, true, false>(orow, tmp, bg, dst, coefs, descs, im, k, ov_w_max);
-        __syncthreads();  // orow is reused by the next entry
-    }
-}
-
-// The fused launch's extra parameters (ipp_pipe_fused).
-struct FusedCfg {
-    int tyv, max_ov_w;
-    int32_t* sync;
-};
 
 template <int NR, bool ZONES, int CN>
-void launch_hpass(dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
-                  const ipp_pipe_desc* descs, int ty, const ipp_hsv_params& hp, const uint8_t* bg, uint8_t* dst,
-                  const FusedCfg* fz) {
-    const int n = grid.x / ty;
-    if (fz) {
-        const int cpi = copy_blocks_per_item();
-        const size_t vb = (size_t)VBR * orow_stride(fz->max_ov_w) * sizeof(uint32_t);
-        if (vb > sizeof(Hpass2Lds<NR>)) {
-            // overlay rows wider than the fused launch's LDS: the split form
-            hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, true>), dim3((uint32_t)(n * (ty + cpi))), dim3(64 * HP_NW),
-                               0, s, src, tmp, coefs, descs, ty, hp, bg, dst, cpi);
-            hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 0, true>), dim3((uint32_t)(n * fz->tyv)), dim3(256), vb, s, tmp,
-                               bg, dst, coefs, descs, fz->tyv, fz->max_ov_w);
-            return;
-        }
-        if (hipMemsetAsync(fz->sync, 0, (size_t)(n + 1) * sizeof(int32_t), s) != hipSuccess) return;
-        hipLaunchKernelGGL((k_pipe_fused<NR, ZONES, CN>), dim3((uint32_t)(n * (ty + cpi + fz->tyv))),
-                           dim3(64 * HP_NW), 0, s, src, tmp, coefs, descs, n, ty, cpi, fz->tyv, hp, bg, dst,
-                           fz->max_ov_w, fz->sync);
-        hipLaunchKernelGGL(k_pipe_vdeferred, dim3((uint32_t)std::min(n * fz->tyv, 2048)), dim3(256), vb, s, tmp, bg,
-                           dst, coefs, descs, n, fz->tyv, fz->max_ov_w, fz->sync);
-        return;
-    }
+void launch_hpass(int n, int ty, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
+                  const ipp_pipe_desc* descs, const ipp_hsv_params& hp, const uint8_t* bg, uint8_t* dst) {
 #ifdef IPP_DIAG
     // diagnostic: unused dynamic LDS per block, to cap the blocks per CU
     static const size_t pad = (size_t)diag_env("IPP_HP_PAD", 0);
 #else
     constexpr size_t pad = 0;
 #endif
-    if (bg && dst) {  // H pass + the background rows outside the overlay bands
-        const int cpi = copy_blocks_per_item();
-        hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, true>), dim3((uint32_t)(n * (ty + cpi))), dim3(64 * HP_NW),
-                           pad, s, src, tmp, coefs, descs, ty, hp, bg, dst, cpi);
-        return;
-    }
-    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN, false>), grid, dim3(64 * HP_NW), pad, s, src, tmp, coefs, descs,
-                       ty, hp, bg, dst, 0);
+    // H pass + the background rows outside the overlay bands
+    const int cpi = copy_blocks_per_item();
+    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), dim3((uint32_t)(n * (ty + cpi))), dim3(64 * HP_NW), pad,
+                       s, src, tmp, coefs, descs, ty, hp, bg, dst, cpi);
 }
 
 template <int NR>
-void launch_hpass_nr(bool zones, int cn, dim3 grid, hipStream_t s, const uint8_t* src, uint8_t* tmp,
-                     const int32_t* coefs, const ipp_pipe_desc* descs, int ty, const ipp_hsv_params& hp,
-                     const uint8_t* bg, uint8_t* dst, const FusedCfg* fz) {
+void launch_hpass_nr(bool zones, int cn, int n, int ty, hipStream_t s, const uint8_t* src, uint8_t* tmp,
+                     const int32_t* coefs, const ipp_pipe_desc* descs, const ipp_hsv_params& hp, const uint8_t* bg,
+                     uint8_t* dst) {
     if (zones) {
-        if (cn == 4) launch_hpass<NR, true, 4>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst, fz);
-        else launch_hpass<NR, true, 3>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst, fz);
+        if (cn == 4) launch_hpass<NR, true, 4>(n, ty, s, src, tmp, coefs, descs, hp, bg, dst);
+        else launch_hpass<NR, true, 3>(n, ty, s, src, tmp, coefs, descs, hp, bg, dst);
     } else {
-        if (cn == 4) launch_hpass<NR, false, 4>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst, fz);
-        else launch_hpass<NR, false, 3>(grid, s, src, tmp, coefs, descs, ty, hp, bg, dst, fz);
+        if (cn == 4) launch_hpass<NR, false, 4>(n, ty, s, src, tmp, coefs, descs, hp, bg, dst);
+        else launch_hpass<NR, false, 3>(n, ty, s, src, tmp, coefs, descs, hp, bg, dst);
     }
 }
 
 }  // namespace
-
-static int pipe_hpass_impl(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
-                           int32_t n_images, int32_t max_out_w, int32_t max_rows, int32_t src_cn,
-                           const ipp_hsv_params* hsv, int32_t tap_format, const uint8_t* bg, uint8_t* dst,
-                           void* stream, const FusedCfg* fz = nullptr) {
-    if (n_images == 0) return IPP_OK;
-    if (!src || !tmp || !coefs || !descs || !hsv || n_images < 0 || max_out_w <= 0 || max_rows <= 0) return IPP_E_ARG;
-    if (src_cn != 3 && src_cn != 4) return IPP_E_ARG;
-    if (tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;  // the VALU dot4 kernels were retired
-    const int ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
-    const int64_t blocks = (int64_t)ty * n_images;
-    if ((int64_t)(ty + (bg ? copy_blocks_per_item() : 0) + (fz ? fz->tyv : 0)) * n_images >= INT32_MAX) return IPP_E_ARG;
-    const dim3 grid((uint32_t)blocks);
-    hipStream_t s = (hipStream_t)stream;
-    // Zones are needed unless every range's zone is the whole image (all
-    // margins 0).  The source channel count is uniform over the batch.
-    bool zones = false;
-    for (int k = 0; k < hsv->n_ranges; ++k)
-        for (int m = 0; m < 4; ++m) zones |= hsv->r[k].zone[m] != 0;
-    const int cn = src_cn;
-    // A range that never matches: lo_v = 1 > hi_v = 0 (cv::inRange's empty range).
-    const ipp_hsv_range never = ipp_hsv_range{{0, 0, 1}, {180, 255, 0}, {0, 0, 0, 0}};
-    switch (hsv->n_ranges) {
-        case 1: launch_hpass_nr<1>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst, fz); break;
-        case 2: launch_hpass_nr<2>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst, fz); break;
-        case 3: launch_hpass_nr<3>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst, fz); break;
-        case 4: launch_hpass_nr<4>(zones, cn, grid, s, src, tmp, coefs, descs, ty, *hsv, bg, dst, fz); break;
-        case 5: case 6: {
-            ipp_hsv_params q = *hsv;  // pad with never-matching ranges (lo > hi in v)
-            for (int k = q.n_ranges; k < 6; ++k) q.r[k] = never;
-            launch_hpass_nr<6>(zones, cn, grid, s, src, tmp, coefs, descs, ty, q, bg, dst, fz);
-            break;
-        }
-        default: {
-            if (hsv->n_ranges > IPP_MAX_HSV_RANGES) return IPP_E_ARG;
-            ipp_hsv_params q = *hsv;
-            for (int k = q.n_ranges; k < IPP_MAX_HSV_RANGES; ++k) q.r[k] = never;
-            launch_hpass_nr<IPP_MAX_HSV_RANGES>(zones, cn, grid, s, src, tmp, coefs, descs, ty, q, bg, dst, fz);
-            break;
-        }
-    }
-    IPP_CHECK_LAUNCH();
-    return IPP_OK;
-}
-
-extern "C" int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
-                              int32_t n_images, int32_t max_out_w, int32_t max_rows, int32_t src_cn,
-                              const ipp_hsv_params* hsv, int32_t tap_format, void* stream) {
-    return pipe_hpass_impl(src, tmp, coefs, descs, n_images, max_out_w, max_rows, src_cn, hsv, tap_format, nullptr,
-                           nullptr, stream);
-}
 
 extern "C" int ipp_pipe_hpass_bgcopy(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                                      const ipp_pipe_desc* descs, int32_t n_images, int32_t max_out_w,
                                      int32_t max_rows, int32_t src_cn, const ipp_hsv_params* hsv,
                                      int32_t tap_format, const uint8_t* bg, uint8_t* dst, void* stream) {
     if (n_images == 0) return IPP_OK;
-    if (!bg || !dst || tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;
-    return pipe_hpass_impl(src, tmp, coefs, descs, n_images, max_out_w, max_rows, src_cn, hsv, tap_format, bg, dst,
-                           stream);
-}
-
-// Bands per item of the fused launch: an overlay of height H at any y spans
-// at most ceil((15 + H) / 16) 16-row bands.
-static int fused_tyv(int32_t bg_h, int32_t max_ov_h) {
-    return std::min((max_ov_h + 15 + VBR - 1) / VBR, (bg_h + VBR - 1) / VBR);
-}
-
-extern "C" int64_t ipp_pipe_sync_bytes(int32_t n_images, int32_t bg_h, int32_t max_ov_h) {
-    if (n_images < 0 || bg_h <= 0 || max_ov_h <= 0) return -1;
-    return (int64_t)sizeof(int32_t) * (1 + n_images + (int64_t)n_images * fused_tyv(bg_h, max_ov_h));
-}
-
-extern "C" int ipp_pipe_fused(const uint8_t* src, uint8_t* tmp, const int32_t* coefs, const ipp_pipe_desc* descs,
-                              int32_t n_images, int32_t max_out_w, int32_t max_rows, int32_t src_cn,
-                              const ipp_hsv_params* hsv, int32_t tap_format, const uint8_t* bg, uint8_t* dst,
-                              int32_t bg_w, int32_t bg_h, int32_t max_ov_w, int32_t max_ov_h, void* sync,
-                              void* stream) {
-    if (n_images == 0) return IPP_OK;
-    if (!bg || !dst || !sync || tap_format != IPP_TAPS_MFMA || bg_w <= 0 || bg_h <= 0) return IPP_E_ARG;
-    if (max_ov_w <= 0 || max_ov_w > bg_w || max_ov_h <= 0 || max_ov_h > bg_h) return IPP_E_ARG;
-    if ((size_t)VBR * orow_stride(max_ov_w) * sizeof(uint32_t) > 64 * 1024) return IPP_E_ARG;
-    const FusedCfg fz{fused_tyv(bg_h, max_ov_h), max_ov_w, reinterpret_cast<int32_t*>(sync)};
-    return pipe_hpass_impl(src, tmp, coefs, descs, n_images, max_out_w, max_rows, src_cn, hsv, tap_format, bg, dst,
-                           stream, &fz);
+    if (!src || !tmp || !coefs || !descs || !hsv || !bg || !dst || n_images < 0 || max_out_w <= 0 || max_rows <= 0)
+        return IPP_E_ARG;
+    if (src_cn != 3 && src_cn != 4) return IPP_E_ARG;
+    if (tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;
+    const int ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
+    if ((int64_t)(ty + copy_blocks_per_item()) * n_images >= INT32_MAX) return IPP_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    // Zones are needed unless every range's zone is the whole image (all
+    // margins 0).  The source channel count is uniform over the batch.
+    bool zones = false;
+    for (int k = 0; k < hsv->n_ranges; ++k)
+        for (int m = 0; m < 4; ++m) zones |= hsv->r[k].zone[m] != 0;
+    const int cn = src_cn, n = n_images;
+    // A range that never matches: lo_v = 1 > hi_v = 0 (cv::inRange's empty range).
+    const ipp_hsv_range never = ipp_hsv_range{{0, 0, 1}, {180, 255, 0}, {0, 0, 0, 0}};
+    switch (hsv->n_ranges) {
+        case 1: launch_hpass_nr<1>(zones, cn, n, ty, s, src, tmp, coefs, descs, *hsv, bg, dst); break;
+        case 2: launch_hpass_nr<2>(zones, cn, n, ty, s, src, tmp, coefs, descs, *hsv, bg, dst); break;
+        case 3: launch_hpass_nr<3>(zones, cn, n, ty, s, src, tmp, coefs, descs, *hsv, bg, dst); break;
+        case 4: launch_hpass_nr<4>(zones, cn, n, ty, s, src, tmp, coefs, descs, *hsv, bg, dst); break;
+        case 5: case 6: {
+            ipp_hsv_params q = *hsv;  // pad with never-matching ranges (lo > hi in v)
+            for (int k = q.n_ranges; k < 6; ++k) q.r[k] = never;
+            launch_hpass_nr<6>(zones, cn, n, ty, s, src, tmp, coefs, descs, q, bg, dst);
+            break;
+        }
+        default: {
+            if (hsv->n_ranges > IPP_MAX_HSV_RANGES) return IPP_E_ARG;
+            ipp_hsv_params q = *hsv;
+            for (int k = q.n_ranges; k < IPP_MAX_HSV_RANGES; ++k) q.r[k] = never;
+            launch_hpass_nr<IPP_MAX_HSV_RANGES>(zones, cn, n, ty, s, src, tmp, coefs, descs, q, bg, dst);
+            break;
+        }
+    }
+    IPP_CHECK_LAUNCH();
+    return IPP_OK;
 }
 
 extern "C" int ipp_pipe_status(int32_t* status, void* stream) {
@@ -1226,39 +1100,20 @@ extern "C" int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint
     const int tyb = std::min((max_ov_h + 15 + VBR - 1) / VBR, (bg_h + VBR - 1) / VBR);
     const int64_t nb = (int64_t)tyb * n_images;
     if (nb >= INT32_MAX || sm > 64 * 1024) return IPP_E_ARG;
-    hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 0, true>), dim3((uint32_t)nb), dim3(256), sm, (hipStream_t)stream, tmp,
-                       bg, dst, coefs, descs, tyb, max_ov_w);
-    IPP_CHECK_LAUNCH();
-    return IPP_OK;
-}
-
-extern "C" int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst, const int32_t* coefs,
-                               const ipp_pipe_desc* descs, int32_t n_images, int32_t bg_w, int32_t bg_h,
-                               int32_t max_ov_w, int32_t tap_format, void* stream) {
-    if (n_images == 0) return IPP_OK;
-    if (!tmp || !bg || !dst || !coefs || !descs || n_images < 0 || bg_w <= 0 || bg_h <= 0) return IPP_E_ARG;
-    if (tap_format != IPP_TAPS_MFMA || max_ov_w <= 0 || max_ov_w > bg_w) return IPP_E_ARG;
-    const size_t sm = (size_t)VBR * orow_stride(max_ov_w) * sizeof(uint32_t);
-    const int tyb = (bg_h + VBR - 1) / VBR;
-    const int64_t nb = (int64_t)tyb * n_images;
-    if (nb >= INT32_MAX || sm > 64 * 1024) return IPP_E_ARG;
-    const dim3 grid((uint32_t)nb);
     hipStream_t st = (hipStream_t)stream;
 #ifdef IPP_DIAG
-    // store policy 0 plain / 1 sc1 / 2 nt; experiment kernels (WRONG output):
-    // 9 no background reads, 10 no V pass, 11 stores only
+    // experiment kernels (WRONG output): 9 no background reads, 10 no V pass, 11 stores only
     static const int pol = diag_env("IPP_VB_STORE", 2);
     switch (pol) {
-        case 0: hipLaunchKernelGGL(k_pipe_vblend_mfma<0>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-        case 1: hipLaunchKernelGGL(k_pipe_vblend_mfma<1>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-        case 9: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 1>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-        case 10: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 2>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-        case 11: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 3>), grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-        default: hipLaunchKernelGGL(k_pipe_vblend_mfma<2>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        case 9: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 1>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        case 10: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 2>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        case 11: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 3>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        default: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 0>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
     }
 #else
     // nt stores: the write-once composite does not evict the shared backgrounds
-    hipLaunchKernelGGL(k_pipe_vblend_mfma<2>, grid, dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w);
+    hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 0>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs,
+                       descs, tyb, max_ov_w);
 #endif
     IPP_CHECK_LAUNCH();
     return IPP_OK;

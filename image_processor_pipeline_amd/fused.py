@@ -12,8 +12,8 @@ The reference runs five ``ProcessingStep``s chained through files
 
 Here one host planning pass draws every random parameter in the reference's
 draw order (``draw_params``) and fills one ``ipp_pipe_desc`` per item; the
-device work is two launches for the whole batch (``ipp_pipe_hpass``,
-``ipp_pipe_vblend``).  Intermediate cut-outs never touch HBM.
+device work is two launches for the whole batch (``ipp_pipe_hpass_bgcopy``,
+``ipp_pipe_vblend_bands``).  Intermediate cut-outs never touch HBM.
 """
 from __future__ import annotations
 
@@ -33,10 +33,6 @@ from .device import SYM_FLIP, _stream, _to_dev
 
 ALL_SYMS = ("o", "h", "v", "hv")
 H_RING_COLUMNS = 512   # ipp_pipe.hip RING
-# Default launch form of a batch: "split" = ipp_pipe_hpass_bgcopy +
-# ipp_pipe_vblend_bands (measured 1-2 % faster on MI355X than the one-launch
-# "fused" = ipp_pipe_fused); both write the same bytes.
-PIPE_FORM = "split"
 
 
 @dataclass
@@ -303,22 +299,6 @@ class PipeRunner:
         self.coefs, self.host_tiles = plan_taps(plan, self.device)
         self.tmp = torch.empty(plan.tmp_bytes, dtype=torch.uint8, device=self.device)
         self.lib = N.load()
-        nb = self.lib.ipp_pipe_sync_bytes(len(plan.descs), plan.bg_h, plan.max_ov_h)
-        if nb < 0:
-            raise N.NativeError(f"ipp_pipe_sync_bytes({len(plan.descs)}, {plan.bg_h}, {plan.max_ov_h}) failed")
-        self.sync = torch.empty(max(int(nb), 4), dtype=torch.uint8, device=self.device)
-
-    def hpass(self, src: torch.Tensor) -> None:
-        p = self.plan
-        N.check(self.lib.ipp_pipe_hpass(src.data_ptr(), self.tmp.data_ptr(), self.coefs.data_ptr(),
-                                        self.descs.data_ptr(), len(p.descs), p.max_out_w, p.max_rows, 3,
-                                        N.np_ptr(p.hsv), p.tap_format, _stream(self.device)), "ipp_pipe_hpass")
-
-    def vblend(self, bgs: torch.Tensor, out: torch.Tensor) -> None:
-        p = self.plan
-        N.check(self.lib.ipp_pipe_vblend(self.tmp.data_ptr(), bgs.data_ptr(), out.data_ptr(), self.coefs.data_ptr(),
-                                         self.descs.data_ptr(), len(p.descs), p.bg_w, p.bg_h, p.max_ov_w,
-                                         p.tap_format, _stream(self.device)), "ipp_pipe_vblend")
 
     def hpass_bgcopy(self, src: torch.Tensor, bgs: torch.Tensor, out: torch.Tensor) -> None:
         """H pass + the composite rows outside the overlay bands (split form)."""
@@ -336,22 +316,6 @@ class PipeRunner:
                                                p.bg_h, p.max_ov_w, p.max_ov_h, p.tap_format,
                                                _stream(self.device)), "ipp_pipe_vblend_bands")
 
-    def fused(self, src: torch.Tensor, bgs: torch.Tensor, out: torch.Tensor) -> None:
-        """The whole pipe in one launch (+ the queued-band launch): H pass,
-        background copy and V pass with paste (ipp_pipe_fused)."""
-        p = self.plan
-        N.check(self.lib.ipp_pipe_fused(src.data_ptr(), self.tmp.data_ptr(), self.coefs.data_ptr(),
-                                        self.descs.data_ptr(), len(p.descs), p.max_out_w, p.max_rows, 3,
-                                        N.np_ptr(p.hsv), p.tap_format, bgs.data_ptr(), out.data_ptr(), p.bg_w,
-                                        p.bg_h, p.max_ov_w, p.max_ov_h, self.sync.data_ptr(),
-                                        _stream(self.device)), "ipp_pipe_fused")
-
-    def queued_bands(self) -> int:
-        """Bands the last fused launch queued for its second launch (not
-        ready when their block started).  Synchronises."""
-        torch.cuda.synchronize(self.device)
-        return int(self.sync[4 * len(self.plan.descs):4 * len(self.plan.descs) + 4].view(torch.int32).item())
-
     def status(self) -> int:
         """Sticky status of the pipe kernels since the last call (ipp_pipe_status;
         bit 0: an H tile's window exceeded the LDS ring).  Synchronises."""
@@ -367,14 +331,10 @@ class PipeRunner:
         for t, name in ((src, "src"), (bgs, "bgs"), (out, "out")):
             if not (t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous()):
                 raise N.NativeUnavailable(f"PipeRunner.run: {name} must be a contiguous uint8 ROCm tensor")
-        if self.split and PIPE_FORM == "fused":
-            self.fused(src, bgs, out)
-        elif self.split:
-            self.hpass_bgcopy(src, bgs, out)
-            self.vblend_bands(bgs, out)
-        else:
-            self.hpass(src)
-            self.vblend(bgs, out)
+        if not self.split:
+            raise N.NativeError(f"PipeRunner.run: tap format {self.plan.tap_format} (the pipe takes IPP_TAPS_MFMA)")
+        self.hpass_bgcopy(src, bgs, out)
+        self.vblend_bands(bgs, out)
         return out
 
 
@@ -383,7 +343,7 @@ class PipeStream:
     own plan, built while the previous batch runs.  A worker thread runs
     batch k+1's host plan (ipp_plan_pipe_batch; ctypes drops the GIL) and
     its device taps (ipp_pipe_plan_taps on a side stream) while batch k's
-    launches (PIPE_FORM) run on the caller's stream.  Device buffers live in
+    two launches run on the pipe stream.  Device buffers live in
     `slots` sets that alternate; a set is refilled only after the batch that
     last used it has completed (its HIP event)."""
 
@@ -414,14 +374,9 @@ class PipeStream:
         plan = self.plan_fn(k)
         t1 = time.perf_counter()
         slot["done"].synchronize()              # the batch that used these buffers has finished
-        n = len(plan.descs)
-        nsync = self.lib.ipp_pipe_sync_bytes(n, plan.bg_h, plan.max_ov_h)
-        if nsync < 0:
-            raise N.NativeError(f"ipp_pipe_sync_bytes({n}, {plan.bg_h}, {plan.max_ov_h}) failed")
         bufs = {"descs": self._buf(slot, "descs", plan.descs.nbytes),
                 "coefs": self._buf(slot, "coefs", 4 * (plan.coef_words + 4096)),
                 "tmp": self._buf(slot, "tmp", plan.tmp_bytes),
-                "sync": self._buf(slot, "sync", nsync),
                 "scratch": self._buf(slot, "scratch", self.lib.ipp_pipe_taps_scratch_bytes(len(plan.axes)))}
         stats = np.zeros(2, np.int64)
         with torch.cuda.stream(self.side):
@@ -456,24 +411,16 @@ class PipeStream:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if record else None
                 if ev:
                     ev[0].record(main)
-                if PIPE_FORM == "fused":
-                    N.check(self.lib.ipp_pipe_fused(src.data_ptr(), b["tmp"].data_ptr(), b["coefs"].data_ptr(),
-                                                    b["descs"].data_ptr(), len(plan.descs), plan.max_out_w,
-                                                    plan.max_rows, 3, N.np_ptr(plan.hsv), plan.tap_format,
-                                                    bgs.data_ptr(), out.data_ptr(), plan.bg_w, plan.bg_h,
-                                                    plan.max_ov_w, plan.max_ov_h, b["sync"].data_ptr(),
-                                                    main.cuda_stream), "ipp_pipe_fused")
-                else:
-                    N.check(self.lib.ipp_pipe_hpass_bgcopy(src.data_ptr(), b["tmp"].data_ptr(), b["coefs"].data_ptr(),
-                                                           b["descs"].data_ptr(), len(plan.descs), plan.max_out_w,
-                                                           plan.max_rows, 3, N.np_ptr(plan.hsv), plan.tap_format,
-                                                           bgs.data_ptr(), out.data_ptr(), main.cuda_stream),
-                            "ipp_pipe_hpass_bgcopy")
-                    N.check(self.lib.ipp_pipe_vblend_bands(b["tmp"].data_ptr(), bgs.data_ptr(), out.data_ptr(),
-                                                           b["coefs"].data_ptr(), b["descs"].data_ptr(),
-                                                           len(plan.descs), plan.bg_w, plan.bg_h, plan.max_ov_w,
-                                                           plan.max_ov_h, plan.tap_format, main.cuda_stream),
-                            "ipp_pipe_vblend_bands")
+                N.check(self.lib.ipp_pipe_hpass_bgcopy(src.data_ptr(), b["tmp"].data_ptr(), b["coefs"].data_ptr(),
+                                                       b["descs"].data_ptr(), len(plan.descs), plan.max_out_w,
+                                                       plan.max_rows, 3, N.np_ptr(plan.hsv), plan.tap_format,
+                                                       bgs.data_ptr(), out.data_ptr(), main.cuda_stream),
+                        "ipp_pipe_hpass_bgcopy")
+                N.check(self.lib.ipp_pipe_vblend_bands(b["tmp"].data_ptr(), bgs.data_ptr(), out.data_ptr(),
+                                                       b["coefs"].data_ptr(), b["descs"].data_ptr(),
+                                                       len(plan.descs), plan.bg_w, plan.bg_h, plan.max_ov_w,
+                                                       plan.max_ov_h, plan.tap_format, main.cuda_stream),
+                        "ipp_pipe_vblend_bands")
                 if ev:
                     ev[1].record(main)
                     self.events.append(ev)

@@ -209,38 +209,27 @@ typedef struct ipp_pipe_desc {
  * IPP_E_ARG. */
 #define IPP_TAPS_MFMA 1   /* 16-output tiles, v_mfma_i32_16x16x64_i8          */
 
-/* src_cn: channels of every source in the batch (3 or 4); hsv: HOST pointer.
+/* The batched 5-stage pipe as two launches (fused.PipeRunner.run, bench.py;
+ * reference chain pipeline.py:526-541 → rotations.py:96, symmetry.py:114-119,
+ * filtres_liste.py:84-134, overlays.py:129,138-139).  A composite's rows
+ * outside the 16-row bands the overlay touches, [16⌊y/16⌋, 16⌈(y + ov_h)/16⌉),
+ * are plain copies of the background (Paste.c leaves them untouched):
+ *   ipp_pipe_hpass_bgcopy: the LANCZOS H pass over the virtual cut-out (crop →
+ *     rotate → flip → HSV α computed per pixel from the source, never stored)
+ *     into the scratch `tmp`, plus the copy of those background rows into
+ *     `dst`, spread over copy blocks that run beside the H-pass blocks;
+ *   ipp_pipe_vblend_bands: the V pass over the overlay bands, fused with the
+ *     unpremultiply, the alpha blend and the rest of each band's background.
+ * src_cn: channels of every source in the batch (3 or 4); hsv: HOST pointer;
+ * tap_format: IPP_TAPS_MFMA (V axes planned with transposed = 2 + (p.y mod
+ * 16), i.e. tap tiles aligned with 16-row background bands); max_ov_w /
+ * max_ov_h bound the overlay sizes.
  * Ring limit: the H pass keeps each 16-output tile's input window in a
  * 512-column LDS ring, so every H tile must satisfy 64·nK ≤ 512 (nK = its K
  * steps; ipp_plan_mfma_nk_bound(in, out, ksize) ≤ 8, i.e. LANCZOS downscales
- * of at most ≈ 23×; fused.plan_pipe refuses plans beyond it).  A violating tile sets bit 0 of the sticky status read by
- * ipp_pipe_status; its T columns are then wrong. */
-int ipp_pipe_hpass(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
-                   const ipp_pipe_desc* descs, int32_t n_images,
-                   int32_t max_out_w, int32_t max_rows, int32_t src_cn,
-                   const ipp_hsv_params* hsv, int32_t tap_format, void* stream);
-/* tap_format: IPP_TAPS_MFMA (V axes planned with transposed = 2 + (p.y mod
- * 16), i.e. tap tiles aligned with 16-row background bands); max_ov_w bounds
- * the overlay widths. */
-int ipp_pipe_vblend(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
-                    const int32_t* coefs, const ipp_pipe_desc* descs, int32_t n_images,
-                    int32_t bg_w, int32_t bg_h, int32_t max_ov_w, int32_t tap_format,
-                    void* stream);
-
-/* Reads and clears the sticky status of the pipe kernels (bit 0: ring limit
- * violated, see ipp_pipe_hpass).  Synchronises `stream`. */
-int ipp_pipe_status(int32_t* status, void* stream);
-
-/* Split form of the pair above (MFMA taps only), used by the batched device
- * mode (fused.PipeRunner.run).  A composite's rows outside the 16-row bands
- * the overlay touches, [16⌊y/16⌋, 16⌈(y + ov_h)/16⌉), are plain copies of the
- * background (Paste.c, overlays.py:138-139, leaves them untouched):
- *   ipp_pipe_hpass_bgcopy = ipp_pipe_hpass + the copy of those rows, spread
- *     over the H-pass blocks of the item (the H pass is VALU-bound and leaves
- *     the memory system idle);
- *   ipp_pipe_vblend_bands = ipp_pipe_vblend restricted to the overlay bands;
- *     max_ov_h bounds the overlay heights.
- * Together they write exactly what ipp_pipe_hpass + ipp_pipe_vblend write. */
+ * of at most ≈ 23×; fused.plan_pipe refuses plans beyond it).  A violating
+ * tile sets bit 0 of the sticky status read by ipp_pipe_status; its T columns
+ * are then wrong. */
 int ipp_pipe_hpass_bgcopy(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                           const ipp_pipe_desc* descs, int32_t n_images,
                           int32_t max_out_w, int32_t max_rows, int32_t src_cn,
@@ -251,25 +240,9 @@ int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint8_t* dst,
                           int32_t bg_w, int32_t bg_h, int32_t max_ov_w, int32_t max_ov_h,
                           int32_t tap_format, void* stream);
 
-/* One-launch form of the split pair (the default of fused.PipeRunner.run and
- * of bench.py; same reference call sites: rotations.py:96, filtres_liste.py:
- * 84-134, overlays.py:129,138-139).  The V-pass bands of item i run inside the
- * H-pass launch, placed a few items after i's H blocks, so the latency-bound V
- * pass overlaps the VALU-bound H pass.  A V band starts only if every H block
- * of its item has finished (a per-item counter in `sync`; T is handed over
- * with write-through stores and cache-bypassing loads); otherwise it is queued
- * and a second launch, issued by this call, runs the queue.  No block waits
- * for another, so correctness does not depend on the dispatch order.
- * sync: device scratch of ipp_pipe_sync_bytes(n_images, bg_h, max_ov_h) bytes
- * (its counters are reset by this call, on `stream`).  Writes exactly what
- * ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands write. */
-int64_t ipp_pipe_sync_bytes(int32_t n_images, int32_t bg_h, int32_t max_ov_h);
-int ipp_pipe_fused(const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
-                   const ipp_pipe_desc* descs, int32_t n_images,
-                   int32_t max_out_w, int32_t max_rows, int32_t src_cn,
-                   const ipp_hsv_params* hsv, int32_t tap_format,
-                   const uint8_t* bg, uint8_t* dst, int32_t bg_w, int32_t bg_h,
-                   int32_t max_ov_w, int32_t max_ov_h, void* sync, void* stream);
+/* Reads and clears the sticky status of the pipe kernels (bit 0: ring limit
+ * violated, see above).  Synchronises `stream`. */
+int ipp_pipe_status(int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* K10-K13: pixels_isolés.keep_largest_component                             */

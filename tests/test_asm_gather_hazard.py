@@ -43,11 +43,11 @@ def _asm_of_build(tmp_path) -> Path:
 @needs_hipcc
 def test_hpass_gathers_never_touched_in_flight(tmp_path, capsys):
     path = _asm_of_build(tmp_path)
-    for pattern, least in (("k_pipe_hpass2", 40), ("k_pipe_fused", 20)):
+    for pattern, least in (("k_pipe_hpass2", 24),):
         rc = asm_hazard.main(str(path), pattern)
         out = capsys.readouterr().out
         n = int(re.search(r"(\d+) kernels checked", out).group(1))
-        assert n >= least, out     # every NR / zones / channels (/ copy) instantiation
+        assert n >= least, out     # every NR / zones / channels instantiation
         assert rc == 0, out        # no in-flight register touched, no scratch
 
 

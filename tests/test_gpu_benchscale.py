@@ -9,9 +9,9 @@ through PipeRunner exactly as bench.py runs it.
 * Every item: the composite rows outside its overlay bands equal its
   background (overlays.py:138-139 leaves them untouched), and rows inside the
   bands equal it outside the overlay's columns.
-* The one-launch form (ipp_pipe_fused) equals the two-launch split form on
-  the whole batch (12.9 GB compared on the device), and no pipe status bit
-  is set.
+* A second run into an output pre-filled with junk writes the same 12.9 GB
+  (compared on the device: every composite byte is written by the two
+  launches, and the run is deterministic), and no pipe status bit is set.
 """
 import sys
 from pathlib import Path
@@ -79,7 +79,7 @@ def test_benchscale_background_outside_overlay(batch):
     assert not bad, bad[:20]
 
 
-def test_benchscale_fused_equals_split(batch):
+def test_benchscale_rerun_is_identical(batch):
     src, bgs, plan, runner, out, cfg = batch
     other = torch.empty_like(out)
     other.fill_(0x5A)

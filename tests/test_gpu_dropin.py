@@ -144,9 +144,8 @@ cfg = fused.PipeConfig(margins=(9, 9, 9, 9))
 r = fused.PipeRunner(fused.plan_pipe((H, W), n, (bh, bw), K, cfg, seed=3), "cuda:0")
 out = torch.empty((n, bh, bw, 3), dtype=torch.uint8, device="cuda:0")
 r.run(src, bgs, out)
-r.hpass(src)
-out2 = torch.empty_like(out)
-r.vblend(bgs, out2)
+out2 = torch.full_like(out, 3)
+r.run(src, bgs, out2)
 g = D.plan_rotate_flip([(H, W, 3)], [33.0], [1])
 rot = D.rotate_flip_nearest(src[0].reshape(-1), g)
 torch.cuda.synchronize()
@@ -160,7 +159,7 @@ def test_diagnostic_env_vars_do_not_change_outputs(tmp_path):
     base = {k: v for k, v in os.environ.items() if not k.startswith("IPP_")}
     digests = []
     for extra in ({}, {"IPP_DBG_HPASS": "11", "IPP_VB_STORE": "9", "IPP_COPY_BLOCKS": "1",
-                       "IPP_GATHER_MAP": "0", "IPP_HPASS": "1", "IPP_TAPS": "dot4"}):
+                       "IPP_GATHER_MAP": "0", "IPP_HPASS": "1", "IPP_HP_PAD": "60000"}):
         p = subprocess.run([sys.executable, str(script), str(ROOT)], capture_output=True, text=True, timeout=180,
                            env=dict(base, **extra))
         assert p.returncode == 0, p.stderr[-2000:]

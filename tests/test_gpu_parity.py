@@ -196,7 +196,7 @@ def test_overlay_reference_chain(D, golden):
         assert np.array_equal(got, comp)
 
 
-# --------------------------------------------------------------------------- fused pipe
+# --------------------------------------------------------------------------- batched pipe
 
 def _run_pipe(n, H, W, K, bh, bw, cfg, seed):
     from image_processor_pipeline_amd import fused
@@ -239,10 +239,11 @@ def test_pipe_structured_content_vs_oracle(D):
         assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), i
 
 
-def test_pipe_split_equals_unsplit(D):
-    """ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands write exactly what
-    ipp_pipe_hpass + ipp_pipe_vblend write; odd background widths take the
-    row-wise copy path (3·bw not a multiple of 16)."""
+def test_pipe_odd_background_widths_vs_oracle(D):
+    """ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands on backgrounds whose row
+    bytes are not a multiple of 16 (the row-wise copy and blend paths) and on
+    aligned ones, output buffers pre-filled with junk: every composite byte
+    is written, and equals the oracle."""
     from image_processor_pipeline_amd import fused
     cfg = fused.PipeConfig(margins=(3, 5, 2, 7), scale_min=0.2, scale_max=0.6)
     for (bh, bw) in [(97, 125), (64, 96)]:
@@ -254,53 +255,17 @@ def test_pipe_split_equals_unsplit(D):
         runner = fused.PipeRunner(plan, DEV)
         assert runner.split
         a = torch.full((n, bh, bw, 3), 7, dtype=torch.uint8, device=DEV)
-        b = torch.full((n, bh, bw, 3), 9, dtype=torch.uint8, device=DEV)
         runner.hpass_bgcopy(_t(src), _t(bgs), a)
         runner.vblend_bands(_t(bgs), a)
-        runner.hpass(_t(src))
-        runner.vblend(_t(bgs), b)
         torch.cuda.synchronize()
-        assert torch.equal(a, b)
         got = a.cpu().numpy()
         for i in range(n):
             assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (bw, i)
 
 
-def test_pipe_fused_equals_split(D):
-    """ipp_pipe_fused (H pass, copy and V bands in one launch, a per-item
-    completion counter, queued bands in a second launch) writes exactly what
-    the two-launch split form writes, for batches small enough that bands are
-    queued (the V blocks of the last items follow their H blocks at once) and
-    larger ones; odd background widths take the row-wise copy path."""
-    from image_processor_pipeline_amd import fused
-    cfg = fused.PipeConfig(margins=(3, 5, 2, 7), scale_min=0.2, scale_max=0.7)
-    queued = 0
-    for (n, bh, bw) in [(1, 97, 125), (3, 64, 96), (40, 120, 160)]:
-        H, W = 90, 110
-        rng = np.random.default_rng(n)
-        src = rng.integers(0, 256, (n, H, W, 3), np.uint8)
-        bgs = rng.integers(0, 256, (3, bh, bw, 3), np.uint8)
-        plan = fused.plan_pipe((H, W), n, (bh, bw), 3, cfg, seed=n)
-        runner = fused.PipeRunner(plan, DEV)
-        a = torch.full((n, bh, bw, 3), 7, dtype=torch.uint8, device=DEV)
-        b = torch.full((n, bh, bw, 3), 9, dtype=torch.uint8, device=DEV)
-        for _ in range(2):  # the second run reuses T and the counters
-            runner.fused(_t(src), _t(bgs), a)
-            queued += runner.queued_bands()
-        runner.hpass_bgcopy(_t(src), _t(bgs), b)
-        runner.vblend_bands(_t(bgs), b)
-        torch.cuda.synchronize()
-        assert torch.equal(a, b), n
-        assert runner.status() == 0
-        got = a.cpu().numpy()
-        for i in range(n):
-            assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (n, i)
-    print("bands queued for the second launch:", queued)
-
-
-def test_pipe_fused_wide_overlay_takes_split_form(D):
-    """Overlay rows wider than the fused launch's LDS (≈ 550 px) make
-    ipp_pipe_fused run the split kernels instead; the bytes are the same."""
+def test_pipe_wide_overlays_vs_oracle(D):
+    """Overlays wider than 560 px (the V pass's overlay rows take most of its
+    64 KB of LDS) on an 800-px background."""
     from image_processor_pipeline_amd import fused
     cfg = fused.PipeConfig(margins=(4, 4, 4, 4), scale_min=0.75, scale_max=0.8)
     n, H, W, bh, bw = 2, 300, 260, 760, 800
@@ -311,21 +276,16 @@ def test_pipe_fused_wide_overlay_takes_split_form(D):
     assert plan.max_ov_w > 560
     runner = fused.PipeRunner(plan, DEV)
     a = torch.full((n, bh, bw, 3), 7, dtype=torch.uint8, device=DEV)
-    b = torch.full((n, bh, bw, 3), 9, dtype=torch.uint8, device=DEV)
-    runner.fused(_t(src), _t(bgs), a)
-    runner.hpass_bgcopy(_t(src), _t(bgs), b)
-    runner.vblend_bands(_t(bgs), b)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b)
+    runner.run(_t(src), _t(bgs), a)
     got = a.cpu().numpy()
     for i in range(n):
         assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), i
 
 
-def test_pipe_stream_both_forms(D, monkeypatch):
-    """fused.PipeStream (bench.py --stream) in both launch forms: every batch
-    has its own plan; the last batch's output equals a PipeRunner run of the
-    same plan."""
+def test_pipe_stream_equals_runner(D):
+    """fused.PipeStream (the bench's streaming leg) on a high-priority and on
+    the default-priority stream: every batch has its own plan; the last
+    batch's output equals a PipeRunner run of the same plan."""
     from image_processor_pipeline_amd import fused
     cfg = fused.PipeConfig(margins=(3, 5, 2, 7), scale_min=0.2, scale_max=0.6)
     n, H, W, bh, bw = 6, 90, 110, 120, 160
@@ -333,14 +293,13 @@ def test_pipe_stream_both_forms(D, monkeypatch):
     src = _t(rng.integers(0, 256, (n, H, W, 3), np.uint8))
     bgs = _t(rng.integers(0, 256, (3, bh, bw, 3), np.uint8))
     plan_fn = lambda k: fused.plan_pipe((H, W), n, (bh, bw), 3, cfg, seed=100 + k)
-    for form, prio in (("split", True), ("fused", True), ("split", False)):
-        monkeypatch.setattr(fused, "PIPE_FORM", form)
+    for prio in (True, False):
         out = torch.empty((n, bh, bw, 3), dtype=torch.uint8, device=DEV)
         fused.PipeStream(DEV, plan_fn, priority=prio).run(3, src, bgs, out, record=True)
         ref = torch.empty_like(out)
         fused.PipeRunner(plan_fn(2), DEV).run(src, bgs, ref)
         torch.cuda.synchronize()
-        assert torch.equal(out, ref), form
+        assert torch.equal(out, ref), prio
 
 
 def test_pipe_crop_reaching_source_end(D):

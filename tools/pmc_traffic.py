@@ -18,13 +18,8 @@ import sys
 from collections import defaultdict
 
 KERNELS = {  # C-ABI entry point → predicate on the (demangled) device kernel name
-    # k_pipe_hpass2<NR, ZONES, CN, DBG, COPY, BANDS>: the copy form has COPY = true
-    "ipp_pipe_hpass_bgcopy": lambda k: "k_pipe_hpass2<" in k and ", true" in k,
-    "ipp_pipe_vblend_bands": lambda k: "k_pipe_vblend_mfma<" in k and ", true>" in k,
-    "ipp_pipe_hpass": lambda k: "k_pipe_hpass" in k and ", true" not in k,
-    "ipp_pipe_vblend": lambda k: "k_pipe_vblend" in k and ", true>" not in k,
-    # one-launch pipe: the fused kernel plus its deferred-band follow-up launch
-    "ipp_pipe_fused": lambda k: "k_pipe_fused" in k or "k_pipe_vdeferred" in k,
+    "ipp_pipe_hpass_bgcopy": lambda k: "k_pipe_hpass" in k,
+    "ipp_pipe_vblend_bands": lambda k: "k_pipe_vblend" in k,
     "ipp_rotate_flip_nearest": lambda k: "k_rotate_flip_nearest" in k,
     "ipp_video_keep_largest": lambda k: "k_ccl" in k or "k_video" in k,
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Profile one bench workload (kernel trace + PMC passes) and record its PMC
-# traffic: tools/gpu_prof2.sh <tag> <workload> <batch-or-frames> [bench args...]
+# traffic: tools/profile_workload.sh <tag> <workload> <batch-or-frames> [bench args...]
 set -o pipefail
 TAG=$1; WL=$2; NB=$3; shift 3
 export TMPDIR=/tmp
