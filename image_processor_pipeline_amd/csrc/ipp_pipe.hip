@@ -87,30 +87,21 @@ __device__ __forceinline__ void pair_regroup(uint32_t (&a)[4], bool o1) {
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-// Cache policy of the H pass's tap loads and of the background copy's loads
-// (experiment switches; 0 = plain loads, 16 = sc1: served by L2, not kept in
-// the CU's L1, which the gathers need).
-#ifndef IPP_TAP_POL
-#define IPP_TAP_POL 0
-#endif
+// Cache policy of the background copy's loads (experiment switch; 0 = plain
+// loads, 16 = sc1: served by L2, not kept in the CU's L1, which the gathers
+// need).
 #ifndef IPP_COPY_POL
 #define IPP_COPY_POL 0
-#endif
-// Tap loads masked to the lanes whose 16 taps can be nonzero (experiment switch).
-#ifndef IPP_TAP_MASK
-#define IPP_TAP_MASK 0
 #endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFFF, 0x00020000);
 }
-template <int POL>
-__device__ __forceinline__ uint4 ld16_pol(const uint4* base, __amdgpu_buffer_rsrc_t rs, int idx) {
+__device__ __forceinline__ uint4 ld_tap(const uint4* base, int idx) {
 #if defined(IPP_DIAG) && defined(IPP_DIAG_NOTAPS)
     // diagnostic (wrong output): no tap loads, constant operands
     { const uint32_t v = (uint32_t)idx * 0x01010101u; asm volatile("" :: "v"(v)); return make_uint4(v, v ^ 1u, v ^ 2u, v ^ 3u); }
 #endif
-    if (POL == 0) return base[idx];
-    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)idx * 16u, 0, POL));
+    return base[idx];
 }
 
 // ---------------------------------------------------------------------------
@@ -147,6 +138,9 @@ struct __attribute__((aligned(16))) Hpass2Lds {
 // M pixel → window byte quad (p | α 255) ^ 0x80 when kept, 0x80808080 (transparent black) when excluded.
 template <int NR, bool ZONES>
 __device__ __forceinline__ uint32_t hsv2_px(const HsvTables<NR>& T, uint32_t raw, uint32_t zbits) {
+#if defined(IPP_DIAG) && defined(IPP_DIAG_NOHSV)
+    return ((raw | 0xFF000000u) ^ 0x80808080u) & (zbits | 0xFFFFFF00u);  // diagnostic (wrong output): no HSV test
+#endif
     uint32_t ex = hsv_tab_excl<NR, false>(T, raw);
     if (ZONES) ex &= zbits;
     const uint32_t t = (raw | 0xFF000000u) ^ 0x80808080u;
@@ -235,6 +229,9 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
             o1 = offc;
         }
         off[k] = ok ? o1 : 0xFFFFFFFFu;
+#if defined(IPP_DIAG) && defined(IPP_DIAG_ALIGNED)
+        off[k] = ok ? (o1 & ~3u) : 0xFFFFFFFFu;  // diagnostic (wrong output): dword-aligned gathers
+#endif
         any |= ok;
         xx += (uint32_t)(2 * B.b0);
         yy += (uint32_t)(2 * B.b3);
@@ -293,11 +290,6 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
     const int32_t* tbias = coefs + h.coef_off + 4 * (int64_t)ntiles;
     const uint4* tblk = reinterpret_cast<const uint4*>(coefs + h.coef_off + 20 * (int64_t)ntiles);
-    const __amdgpu_buffer_rsrc_t brs = rsrc_of(tblk);
-    // Pillow's LANCZOS support in M columns (Resample.c precompute_coeffs:
-    // center (o + 0.5)·scale, support 3·max(scale, 1)), for the tap lane masks
-    const float scale = (float)h.in_len / (float)h.out_len;
-    const float support = 3.0f * fmaxf(scale, 1.0f);
     const uint32_t sx = (uint32_t)HP_STEPC * (uint32_t)B.b0, sy = (uint32_t)HP_STEPC * (uint32_t)B.b3;  // per-step advance
 
     int filled = hdr[0].x;  // ring holds M columns [.., filled)
@@ -334,28 +326,18 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         const bool has_tile = t < ck.s1 && nrows > 0;
         int4 th = make_int4(0, 0, 0, 0);
         uint4 bn[3];
-        float tap_lo, tap_hi;  // the lane's K-step starts with nonzero taps lie in (tap_lo, tap_hi)
         int32_t bias = 0;  // the lane's output column bias, in flight with the taps
         {
             // Loaded unconditionally (a valid tile stands in when the wave
             // has none), so the loads in flight do not depend on the path.
             const int te = min(t, ntiles - 1);
             th = hdr[te];
-            // The lane's 16 taps of a K step are zero outside its output's
-            // support; those lanes load nothing (masked) and take zeros.
-            tap_lo = -1e30f;
-            tap_hi = 1e30f;
-            if (IPP_TAP_MASK) {
-                const float c = ((float)(16 * te + (lane & 15)) + 0.5f) * scale;
-                tap_lo = c - support - 2.0f - (float)(16 * (lane >> 4) + 16);
-                tap_hi = c + support + 2.0f - (float)(16 * (lane >> 4));
-            }
-            const bool act0 = (float)th.x < tap_hi && (float)th.x > tap_lo;
+            // wave-uniform: kept in SGPRs
+            th.x = __builtin_amdgcn_readfirstlane(th.x);
+            th.y = __builtin_amdgcn_readfirstlane(th.y);
+            th.z = __builtin_amdgcn_readfirstlane(th.z);
 #pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                bn[p] = make_uint4(0u, 0u, 0u, 0u);
-                if (act0) bn[p] = ld16_pol<IPP_TAP_POL>(tblk, brs, th.z + lane + p * 64);
-            }
+            for (int p = 0; p < 3; ++p) bn[p] = ld_tap(tblk, th.z + lane + p * 64);
             const int xb = 16 * te + (lane & 15);
             bias = tbias[min(xb, h.out_len - 1)];
             if (!has_tile) th.y = 0;
@@ -468,13 +450,8 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
 #pragma unroll
                 for (int p = 0; p < 3; ++p) bq[p] = __builtin_bit_cast(i32x4, bn[p]);
                 if (ks + 1 < th.y) {
-                    const float kg = (float)(th.x + 64 * (ks + 1));
-                    const bool act = kg < tap_hi && kg > tap_lo;
 #pragma unroll
-                    for (int p = 0; p < 3; ++p) {
-                        bn[p] = make_uint4(0u, 0u, 0u, 0u);
-                        if (act) bn[p] = ld16_pol<IPP_TAP_POL>(tblk, brs, th.z + lane + ((ks + 1) * 3 + p) * 64);
-                    }
+                    for (int p = 0; p < 3; ++p) bn[p] = ld_tap(tblk, th.z + lane + ((ks + 1) * 3 + p) * 64);
                 }
                 const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
 #pragma unroll
