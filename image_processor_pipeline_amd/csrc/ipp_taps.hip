@@ -5,10 +5,11 @@
 // bias[16T] and the i8 B/A blocks, tile t's blocks at uint4 offset t·nkb·192.
 // The taps are Pillow's LANCZOS taps (Resample.c precompute_coeffs +
 // normalize_coeffs_8bpc, reference call site overlays.py:129), computed in
-// fp64 exactly as the host code computes them except for sin(): this file is
+// fp64 as the host code computes them except for the filter's sines (a short
+// series, d_sinpi) and the normalisation (a multiply by 1/ww): this file is
 // compiled with -ffp-contract=off, so every other operation (bounds, filter
-// argument, running sum, division, quantisation) rounds as on the host.  The
-// device sin and libm's differ by at most an ulp or so, which moves a
+// argument, running sum, quantisation) rounds as on the host.  Those two
+// differ from the host's libm sin and division by a few ulps, which moves a
 // quantised tap's pre-truncation value v·2^22 ± 0.5 by < 1e-8; a tile with any
 // tap whose value lies within 2^-22 of an integer is listed and rebuilt on the
 // host with libm (ipp_plan_mfma_tile), so the result is bit-exact.
@@ -36,14 +37,48 @@ constexpr int TAP_CACHE = 64;       // cached weights per output (more: recomput
 constexpr int TAP_FLAG_CAP = 1 << 16;
 constexpr double TAP_NEAR = 1.0 / 4194304.0;  // 2^-22
 
-__device__ inline double d_sinc(double x) {
-    if (x == 0.0) return 1.0;
-    x = x * M_PI;
-    return sin(x) / x;
+// sin(π t) for |t| ≤ 1.5: t = n/2 + f with |f| ≤ 1/4 (exact), then the
+// Taylor series of sin(π f) / cos(π f) to ~1e-17.  A few ulps from libm's
+// sin(fl(π x)), far inside the 2^-22 margin of the near-boundary check below
+// (a deviation δ of a weight moves the quantised value by 2^22 δ / ww).
+__device__ inline double d_sinpi(double t) {
+    const double n = rint(2.0 * t);
+    const double f = t - 0.5 * n;
+    const double x = M_PI * f, z = x * x;
+    double sp = 1.0 / 355687428096000.0;             // 1/17!
+    sp = sp * z - 1.0 / 1307674368000.0;              // 1/15!
+    sp = sp * z + 1.0 / 6227020800.0;                 // 1/13!
+    sp = sp * z - 1.0 / 39916800.0;
+    sp = sp * z + 1.0 / 362880.0;
+    sp = sp * z - 1.0 / 5040.0;
+    sp = sp * z + 1.0 / 120.0;
+    sp = sp * z - 1.0 / 6.0;
+    sp = x + x * z * sp;
+    double cp = 1.0 / 6402373705728000.0;            // 1/18!
+    cp = cp * z - 1.0 / 20922789888000.0;             // 1/16!
+    cp = cp * z + 1.0 / 87178291200.0;                // 1/14!
+    cp = cp * z - 1.0 / 479001600.0;
+    cp = cp * z + 1.0 / 3628800.0;
+    cp = cp * z - 1.0 / 40320.0;
+    cp = cp * z + 1.0 / 720.0;
+    cp = cp * z - 1.0 / 24.0;
+    cp = cp * z + 0.5;
+    cp = 1.0 - z * cp;
+    const int q = (int)n & 3;
+    const double r = (q & 1) ? cp : sp;
+    return (q & 2) ? -r : r;
 }
 
+// Pillow's lanczos(x) = sinc(x) sinc(x / 3), sinc(x) = sin(π x) / (π x), with
+// sin(π x) = sin(3 θ) = s (3 - 4 s²), s = sin(θ), θ = π x / 3: one series.
 __device__ inline double d_lanczos(double x) {
-    if (-3.0 <= x && x < 3.0) return d_sinc(x) * d_sinc(x / 3);
+    if (-3.0 <= x && x < 3.0) {
+        if (x == 0.0) return 1.0;
+        const double t = x / 3;
+        const double s3 = d_sinpi(t);
+        const double s1 = s3 * (3.0 - 4.0 * s3 * s3);
+        return (s1 * s3) / ((x * M_PI) * (t * M_PI));
+    }
     return 0.0;
 }
 
@@ -151,6 +186,7 @@ __global__ __launch_bounds__(256) void k_plan_taps(const ipp_tap_axis* __restric
         // ---- chunks of output col at K offset 64s + 16seg ------------------
         int64_t sum = 0;
         bool near = false;
+        const double rww = ww != 0.0 ? 1.0 / ww : 1.0;  // (a few ulps from v / ww: see d_sinpi)
         for (int s = 0; s < nK; ++s) {
             uint32_t P[3][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
             const int qb = K0 + 64 * s + 16 * seg - xs;
@@ -164,7 +200,7 @@ __global__ __launch_bounds__(256) void k_plan_taps(const ipp_tap_axis* __restric
                         k = 1 << 22;
                     } else {
                         double v = q < TAP_CACHE ? wc[col * TAP_CACHE + q] : d_weight(q, xmin, center, ss);
-                        if (ww != 0.0) v = v / ww;
+                        v = v * rww;
                         const double x = v < 0 ? -0.5 + v * 4194304.0 : 0.5 + v * 4194304.0;
                         k = (int32_t)x;
                         near |= fabs(x - rint(x)) < TAP_NEAR;
@@ -196,11 +232,28 @@ __global__ __launch_bounds__(256) void k_plan_taps(const ipp_tap_axis* __restric
 
 inline int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
 
+// Host-rebuilt tiles are uploaded in one packed copy and put in place by one
+// launch (instead of two small pageable copies per tile, which cost ≈ 0.1 ms
+// each).  Pack: int64 count, int64 record offsets, then per record
+// {int64 bias word offset, int64 block word offset, int64 block bytes, pad},
+// 16 bias words and the blocks, every record 16-byte aligned.
+constexpr int64_t TAP_PACK_BYTES = 4 << 20;
+
+__global__ __launch_bounds__(256) void k_put_tiles(const uint8_t* __restrict__ pack, int32_t* __restrict__ coefs) {
+    const int64_t* hdr = reinterpret_cast<const int64_t*>(pack);
+    const uint8_t* rec = pack + hdr[1 + blockIdx.x];
+    const int64_t* m = reinterpret_cast<const int64_t*>(rec);
+    const uint4* b = reinterpret_cast<const uint4*>(rec + 32);
+    if (threadIdx.x < 4) reinterpret_cast<uint4*>(coefs + m[0])[threadIdx.x] = b[threadIdx.x];
+    uint4* d = reinterpret_cast<uint4*>(coefs + m[1]);
+    for (int64_t i = threadIdx.x; i < m[2] / 16; i += 256) d[i] = b[4 + i];
+}
+
 }  // namespace
 
 extern "C" int64_t ipp_pipe_taps_scratch_bytes(int32_t n_axes) {
     if (n_axes <= 0) return IPP_E_ARG;
-    return align256((int64_t)n_axes * (int64_t)sizeof(ipp_tap_axis)) + 256 + 8 * (int64_t)TAP_FLAG_CAP;
+    return align256((int64_t)n_axes * (int64_t)sizeof(ipp_tap_axis)) + 256 + 8 * (int64_t)TAP_FLAG_CAP + TAP_PACK_BYTES;
 }
 
 extern "C" int ipp_pipe_plan_taps(const ipp_tap_axis* axes, int32_t n_axes, int32_t* coefs, void* scratch,
@@ -252,17 +305,49 @@ extern "C" int ipp_pipe_plan_taps(const ipp_tap_axis* axes, int32_t n_axes, int3
         if (e) return e;
     }
     int rc = IPP_OK;
-    for (size_t i = 0; i < fl.size() && rc == IPP_OK; ++i) {
-        const ipp_tap_axis& a = axes[fl[i].x];
-        const int t = fl[i].y;
-        const int32_t* hdr = hdrs.data() + 4 * i;
-        int32_t* base = coefs + a.coef_off;
-        if (hipMemcpyAsync(base + 4 * (int64_t)a.n_tiles + 16 * t, bias.data() + 16 * i, 64, hipMemcpyHostToDevice,
-                           s) != hipSuccess ||
-            hipMemcpyAsync(base + 20 * (int64_t)a.n_tiles + 4 * (int64_t)hdr[2],
-                           blocks.data() + i * (size_t)maxnk * 3072, (size_t)hdr[1] * 3072, hipMemcpyHostToDevice,
-                           s) != hipSuccess)
+    // one packed upload + one launch when the rebuilt tiles fit the pack region
+    std::vector<int64_t> recoff(fl.size());
+    int64_t pbytes = (8 * (1 + (int64_t)fl.size()) + 15) & ~(int64_t)15;
+    for (size_t i = 0; i < fl.size(); ++i) {
+        recoff[i] = pbytes;
+        pbytes += 32 + 64 + (int64_t)hdrs[4 * i + 1] * 3072;
+    }
+    std::vector<uint8_t> pack;
+    if (pbytes <= TAP_PACK_BYTES) {
+        pack.assign((size_t)pbytes, 0);
+        int64_t* ph = reinterpret_cast<int64_t*>(pack.data());
+        ph[0] = (int64_t)fl.size();
+        for (size_t i = 0; i < fl.size(); ++i) {
+            const ipp_tap_axis& a = axes[fl[i].x];
+            const int t = fl[i].y;
+            ph[1 + i] = recoff[i];
+            int64_t* m = reinterpret_cast<int64_t*>(pack.data() + recoff[i]);
+            m[0] = a.coef_off + 4 * (int64_t)a.n_tiles + 16 * t;
+            m[1] = a.coef_off + 20 * (int64_t)a.n_tiles + 4 * (int64_t)hdrs[4 * i + 2];
+            m[2] = (int64_t)hdrs[4 * i + 1] * 3072;
+            memcpy(pack.data() + recoff[i] + 32, bias.data() + 16 * i, 64);
+            memcpy(pack.data() + recoff[i] + 96, blocks.data() + i * (size_t)maxnk * 3072, (size_t)m[2]);
+        }
+        uint8_t* d_pack = reinterpret_cast<uint8_t*>(d_flags + TAP_FLAG_CAP);
+        if (hipMemcpyAsync(d_pack, pack.data(), (size_t)pbytes, hipMemcpyHostToDevice, s) != hipSuccess) {
             rc = IPP_E_LAUNCH;
+        } else {
+            hipLaunchKernelGGL(k_put_tiles, dim3((uint32_t)fl.size()), dim3(256), 0, s, d_pack, coefs);
+            if (hipGetLastError() != hipSuccess) rc = IPP_E_LAUNCH;
+        }
+    } else {
+        for (size_t i = 0; i < fl.size() && rc == IPP_OK; ++i) {
+            const ipp_tap_axis& a = axes[fl[i].x];
+            const int t = fl[i].y;
+            const int32_t* hdr = hdrs.data() + 4 * i;
+            int32_t* base = coefs + a.coef_off;
+            if (hipMemcpyAsync(base + 4 * (int64_t)a.n_tiles + 16 * t, bias.data() + 16 * i, 64,
+                               hipMemcpyHostToDevice, s) != hipSuccess ||
+                hipMemcpyAsync(base + 20 * (int64_t)a.n_tiles + 4 * (int64_t)hdr[2],
+                               blocks.data() + i * (size_t)maxnk * 3072, (size_t)hdr[1] * 3072, hipMemcpyHostToDevice,
+                               s) != hipSuccess)
+                rc = IPP_E_LAUNCH;
+        }
     }
     if (hipStreamSynchronize(s) != hipSuccess) return IPP_E_LAUNCH;
     return rc;
