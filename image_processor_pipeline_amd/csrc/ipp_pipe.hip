@@ -290,6 +290,15 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
     const int32_t* tbias = coefs + h.coef_off + 4 * (int64_t)ntiles;
     const uint4* tblk = reinterpret_cast<const uint4*>(coefs + h.coef_off + 20 * (int64_t)ntiles);
+#if defined(IPP_DIAG) && defined(IPP_DIAG_TAPSHARE)
+    // diagnostic (wrong output): every block's tap loads read the first item's
+    // blocks (same instructions, L1/L2-resident lines)
+    const uint4* tblk_d = reinterpret_cast<const uint4*>(coefs + 20 * (int64_t)ntiles);
+#define IPP_TAP_INDEX(i) (((i) & 1023))
+#else
+#define IPP_TAP_INDEX(i) (i)
+    const uint4* tblk_d = tblk;
+#endif
     const uint32_t sx = (uint32_t)HP_STEPC * (uint32_t)B.b0, sy = (uint32_t)HP_STEPC * (uint32_t)B.b3;  // per-step advance
 
     int filled = hdr[0].x;  // ring holds M columns [.., filled)
@@ -337,7 +346,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             th.y = __builtin_amdgcn_readfirstlane(th.y);
             th.z = __builtin_amdgcn_readfirstlane(th.z);
 #pragma unroll
-            for (int p = 0; p < 3; ++p) bn[p] = ld_tap(tblk, th.z + lane + p * 64);
+            for (int p = 0; p < 3; ++p) bn[p] = ld_tap(tblk_d, IPP_TAP_INDEX(th.z + lane + p * 64));
             const int xb = 16 * te + (lane & 15);
             bias = tbias[min(xb, h.out_len - 1)];
             if (!has_tile) th.y = 0;
@@ -451,7 +460,12 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                 for (int p = 0; p < 3; ++p) bq[p] = __builtin_bit_cast(i32x4, bn[p]);
                 if (ks + 1 < th.y) {
 #pragma unroll
-                    for (int p = 0; p < 3; ++p) bn[p] = ld_tap(tblk, th.z + lane + ((ks + 1) * 3 + p) * 64);
+                    for (int p = 0; p < 3; ++p) {
+#if defined(IPP_DIAG) && defined(IPP_DIAG_TAPHALF)
+                        if (ks + 1 < 2) continue;  // diagnostic (wrong output): K step 1 reuses step 0's taps
+#endif
+                        bn[p] = ld_tap(tblk_d, IPP_TAP_INDEX(th.z + lane + ((ks + 1) * 3 + p) * 64));
+                    }
                 }
                 const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
 #pragma unroll
