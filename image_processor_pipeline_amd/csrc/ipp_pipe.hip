@@ -236,8 +236,18 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
         xx += (uint32_t)(2 * B.b0);
         yy += (uint32_t)(2 * B.b3);
     }
+#if defined(IPP_DIAG) && defined(IPP_DIAG_NOGATHER)
+    // diagnostic (wrong output): no gathers, pixel values from the offsets
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { o.p[k] = off[k] * 0x9E3779B1u; asm volatile("" : "+v"(o.p[k])); }
+#elif defined(IPP_DIAG) && defined(IPP_DIAG_GATHER_L1)
+    // diagnostic (wrong output): the same gathers folded into a 16 KB window
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o.p[k] = asm_gather(B.rsv, off[k] == 0xFFFFFFFFu ? off[k] : (off[k] & 0x3FFFu));
+#else
 #pragma unroll
     for (int k = 0; k < 4; ++k) o.p[k] = asm_gather(B.rsv, off[k]);
+#endif
     o.any = any;
     o.live = true;
 }
@@ -444,7 +454,11 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // B = 64 columns × 16 outputs of one tap byte plane.  D lane l =
         // output l&15, rows 4(l>>4)..+3 = exactly one 16-B T group.  The
         // column bias rides in the first byte plane's initial accumulator.
+#if defined(IPP_DIAG) && defined(IPP_DIAG_NOPH2)
+        if (has_tile && nrows < 0) {  // diagnostic (wrong output): no MFMA phase
+#else
         if (has_tile) {
+#endif
             i32x4 acc[4][3];
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -694,7 +708,9 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
     const int im = b / per_item;
     const int tb = b - im * per_item;
     if (tb >= tiles_y) {
+#if !(defined(IPP_DIAG) && defined(IPP_DIAG_NOCOPY))  // diagnostic (wrong output): no background copy
         bg_copy_outside_bands<64 * HP_NW>(descs[im].p, bg, dst, tb - tiles_y, cpi);
+#endif
         return;
     }
 #if defined(IPP_DIAG) && defined(IPP_DIAG_COPY_ONLY)

@@ -20,13 +20,14 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 enum Shape { RAND_DW_AL, RAND_DW_UN, RAND_X2_AL, RAND_X2_UN, RAND_X4_AL, RAND_X4_UN, RAND_DW_E32, RAND_DW_E16,
-             BCAST_DW, CONTIG_DW, CONTIG_X4, ROWS16_DW_UN, ROWS16_X2_UN, ROWS16_X4_UN, NSHAPE };
+             BCAST_DW, CONTIG_DW, CONTIG_X4, ROWS16_DW_UN, ROWS16_X2_UN, ROWS16_X4_UN, CONTIG_X4_E16, CONTIG_X4_E32, CONTIG_X2, NSHAPE };
 const char* kName[NSHAPE] = {"rand dword aligned", "rand dword unaligned", "rand dwordx2 aligned",
                              "rand dwordx2 unaligned", "rand dwordx4 aligned", "rand dwordx4 unaligned",
                              "rand dword, 32 lanes", "rand dword, 16 lanes", "broadcast dword",
                              "contiguous dword (256 B)", "contiguous dwordx4 (1 KB)",
                              "16 rows x 4 px dword (H-pass quad map)", "16 rows x 4 px dwordx2",
-                             "16 rows x 4 px dwordx4"};
+                             "16 rows x 4 px dwordx4", "contiguous dwordx4, 16 lanes", "contiguous dwordx4, 32 lanes",
+                             "contiguous dwordx2 (512 B)"};
 
 __device__ __forceinline__ uint32_t hash(uint32_t x) {
     x ^= x >> 16;
@@ -43,7 +44,7 @@ __global__ void __launch_bounds__(256) k_probe(const uint8_t* __restrict__ buf, 
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, 16384 + 64, 0x00020000);
     uint32_t acc = 0;
     uint32_t seed = hash(blockIdx.x * 256 + threadIdx.x);
-    const bool act = S == RAND_DW_E32 ? lane < 32 : (S == RAND_DW_E16 ? lane < 16 : true);
+    const bool act = (S == RAND_DW_E32 || S == CONTIG_X4_E32) ? lane < 32 : ((S == RAND_DW_E16 || S == CONTIG_X4_E16) ? lane < 16 : true);
     uint32_t r0[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) r0[k] = hash(seed + (uint32_t)k * 0x9E3779B9u);
@@ -58,8 +59,9 @@ __global__ void __launch_bounds__(256) k_probe(const uint8_t* __restrict__ buf, 
             uint32_t o;
             if (S == BCAST_DW) o = (u & 255u) * 64u;
             else if (S == CONTIG_DW) o = (u & 63u) * 256u + (uint32_t)lane * 4u;
-            else if (S == CONTIG_X4) o = (u & 15u) * 1024u + (uint32_t)lane * 16u;
-            else if (S >= ROWS16_DW_UN) {
+            else if (S == CONTIG_X4 || S == CONTIG_X4_E16 || S == CONTIG_X4_E32) o = (u & 15u) * 1024u + (uint32_t)lane * 16u;
+            else if (S == CONTIG_X2) o = (u & 31u) * 512u + (uint32_t)lane * 8u;
+            else if (S >= ROWS16_DW_UN && S <= ROWS16_X4_UN) {
                 // lane quad = 2x2 pixels, 16 rows x 4 columns of a 3-byte image of pitch 300 B,
                 // window origin moving per instruction (uniform)
                 const uint32_t org = ((u * 7u) % 40u) * 300u + ((u * 13u) % 60u) * 3u;
@@ -73,10 +75,10 @@ __global__ void __launch_bounds__(256) k_probe(const uint8_t* __restrict__ buf, 
         if (act) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                if (S == RAND_X2_AL || S == RAND_X2_UN || S == ROWS16_X2_UN) {
+                if (S == RAND_X2_AL || S == RAND_X2_UN || S == ROWS16_X2_UN || S == CONTIG_X2) {
                     const u32x2 v = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off[k], 0, 0));
                     acc += v.x ^ v.y;
-                } else if (S == RAND_X4_AL || S == RAND_X4_UN || S == CONTIG_X4 || S == ROWS16_X4_UN) {
+                } else if (S == RAND_X4_AL || S == RAND_X4_UN || S == CONTIG_X4 || S == ROWS16_X4_UN || S == CONTIG_X4_E16 || S == CONTIG_X4_E32) {
                     const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off[k], 0, 0));
                     acc += v.x ^ v.y ^ v.z ^ v.w;
                 } else {
@@ -139,6 +141,9 @@ int main() {
     one<ROWS16_DW_UN>(buf, out, blocks, iters, cus);
     one<ROWS16_X2_UN>(buf, out, blocks, iters, cus);
     one<ROWS16_X4_UN>(buf, out, blocks, iters, cus);
+    one<CONTIG_X4_E32>(buf, out, blocks, iters, cus);
+    one<CONTIG_X4_E16>(buf, out, blocks, iters, cus);
+    one<CONTIG_X2>(buf, out, blocks, iters, cus);
     hipFree(buf);
     hipFree(out);
     return 0;
