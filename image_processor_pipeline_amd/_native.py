@@ -103,7 +103,7 @@ PIPE_ITEM = np.dtype([
 
 TAP_AXIS = np.dtype([
     ("in_size", _I4), ("out_size", _I4), ("identity", _I4), ("shift", _I4), ("phase", _I4), ("nkb", _I4),
-    ("tile0", _I4), ("n_tiles", _I4), ("coef_off", _I8),
+    ("compact", _I4), ("n_tiles", _I4), ("coef_off", _I8),
 ], align=True)
 
 # ipp_plan_pipe_batch totals[] slots (ipp.h IPP_PT_*)

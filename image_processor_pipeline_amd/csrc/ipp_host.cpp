@@ -321,11 +321,27 @@ extern "C" int ipp_plan_mfma_tile(const ipp_tap_axis* a, int32_t t, int32_t hdr[
     for (int o = oa; o < o1; ++o) end = std::max(end, xs[o - o0] + cn[o - o0]);
     const int nK = (end - K0 + 63) / 64;
     if (nK > a->nkb || (int64_t)nK * 3072 > blocks_cap) return IPP_E_RANGE;
+    // compact layout (ipp.h): each output's nonzero 16-column groups
+    int g0[16], len[16], base[16], nb = 0;
+    for (int col = 0; col < 16; ++col) {
+        const int o = o0 + col;
+        const bool valid = o >= oa && o < o1 && cn[col] > 0;
+        g0[col] = valid ? (xs[col] - K0) >> 4 : 0;
+        len[col] = valid ? ((xs[col] + cn[col] - 1 - K0) >> 4) - g0[col] + 1 : 0;
+        base[col] = nb;
+        nb += len[col];
+    }
+    const bool compact = a->compact && !a->identity && nK >= 2 && nb <= 64;
     hdr[0] = K0;
     hdr[1] = nK;
     hdr[2] = t * a->nkb * 192;
-    hdr[3] = 0;
+    hdr[3] = compact ? 1 : 0;
     memset(blocks, 0, (size_t)nK * 3072);
+    if (compact)
+        for (int col = 0; col < 16; ++col) {
+            const int32_t m = g0[col] | len[col] << 8 | base[col] << 16;
+            memcpy(blocks + 4 * col, &m, 4);
+        }
     for (int col = 0; col < 16; ++col) {
         const int o = o0 + col;
         if (o < oa || o >= o1) {
@@ -338,9 +354,15 @@ extern "C" int ipp_plan_mfma_tile(const ipp_tap_axis* a, int32_t t, int32_t hdr[
             sum += k;
             int8_t b[3];
             balanced_bytes(k, b);
-            const int rel = xs[col] + q - K0, s = rel / 64, kin = rel % 64;
-            const int lane = 16 * (kin / 16) + col, j = kin % 16;
-            for (int p = 0; p < 3; ++p) blocks[((int64_t)(s * 3 + p) * 64 + lane) * 16 + j] = (uint8_t)b[p];
+            const int rel = xs[col] + q - K0;
+            if (compact) {
+                const int i = base[col] + (rel >> 4) - g0[col], j = rel & 15;
+                for (int p = 0; p < 3; ++p) blocks[64 + ((int64_t)p * 64 + i) * 16 + j] = (uint8_t)b[p];
+            } else {
+                const int s = rel / 64, kin = rel % 64;
+                const int lane = 16 * (kin / 16) + col, j = kin % 16;
+                for (int p = 0; p < 3; ++p) blocks[((int64_t)(s * 3 + p) * 64 + lane) * 16 + j] = (uint8_t)b[p];
+            }
         }
         bias[col] = (int32_t)((1 << 21) + 128 * sum);
     }

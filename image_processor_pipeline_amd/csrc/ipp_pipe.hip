@@ -345,6 +345,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         const bool has_tile = t < ck.s1 && nrows > 0;
         int4 th = make_int4(0, 0, 0, 0);
         uint4 bn[3];
+        int32_t meta = 0;  // compact tiles: g0 | len << 8 | base << 16 of the lane's output
         int32_t bias = 0;  // the lane's output column bias, in flight with the taps
         {
             // Loaded unconditionally (a valid tile stands in when the wave
@@ -355,12 +356,15 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             th.x = __builtin_amdgcn_readfirstlane(th.x);
             th.y = __builtin_amdgcn_readfirstlane(th.y);
             th.z = __builtin_amdgcn_readfirstlane(th.z);
+            th.w = __builtin_amdgcn_readfirstlane(th.w);
+            // Compact tiles (th.w, ipp.h): meta[16] then one 64-block array
+            // per plane — one load per plane for every K step.  Dense tiles:
+            // the first K step's blocks (meta then reads tap bytes, unused).
 #pragma unroll
-            for (int p = 0; p < 3; ++p) bn[p] = ld_tap(tblk_d, IPP_TAP_INDEX(th.z + lane + p * 64));
-            const int xb = 16 * te + (lane & 15);
-            bias = tbias[min(xb, h.out_len - 1)];
+            for (int p = 0; p < 3; ++p) bn[p] = ld_tap(tblk_d, IPP_TAP_INDEX(th.z + (th.w ? 4 : 0) + lane + p * 64));
             if (!has_tile) th.y = 0;
         }
+        const int te = min(t, ntiles - 1);
 
         // Phase 1: new M columns → planar LDS ring.  Three register sets
         // rotate so that each step's gathers have two steps of HSV work to land.
@@ -426,15 +430,16 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             process(RC, st + 2, 4 * (RA.live + RB.live));
         }
 
-        // The chunk's first tap and bias loads (issued before its gathers) are
-        // waited for here on every path: a compiler wait for them after the
-        // next chunk's asm gathers would drain those as well.
-        asm volatile("" ::"v"(bn[0].x), "v"(bn[1].x), "v"(bn[2].x), "v"(bias));
-        // Next chunk's first steps, issued now so they fly during phase 2
-        // (whose K-step tap loads, issued after them, then wait for them too:
-        // vmcnt retires in order).  (Issuing them after the MFMAs, with the
-        // accumulators live, let the compiler move the in-flight gather
-        // registers and broke parity.)
+        // The chunk's first tap loads (issued before its gathers) and the bias
+        // and meta loads below are waited for on every path before the next
+        // chunk's gathers: a compiler wait for them after those asm gathers
+        // would drain the gathers as well.
+        // The phase-2 column bias and (compact tiles) the lane's group meta,
+        // loaded only now: in flight during phase 1 they cost the registers
+        // that phase 1 needs.  Their latency overlaps the next chunk's header
+        // reads below.
+        meta = reinterpret_cast<const int32_t*>(tblk + th.z)[lane & 15];
+        bias = tbias[min(16 * te + (lane & 15), h.out_len - 1)];
         const int s1 = ck.s1;
         const bool more = s1 < ntiles;
         if (more) {
@@ -445,6 +450,12 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         } else {
             ck.nsteps = 0;  // no loads
         }
+        asm volatile("" ::"v"(bn[0].x), "v"(bn[1].x), "v"(bn[2].x), "v"(bias), "v"(meta));
+        // Next chunk's first steps, issued now so they fly during phase 2
+        // (whose K-step tap loads, issued after them, then wait for them too:
+        // vmcnt retires in order).  (Issuing them after the MFMAs, with the
+        // accumulators live, let the compiler move the in-flight gather
+        // registers and broke parity.)
         issue(ck, 0, xxl, yyl, RA);
         issue(ck, 1, xxl + sx, yyl + sy, RB);
         __syncthreads();
@@ -467,27 +478,56 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                 acc[c][2] = i32x4{0, 0, 0, 0};
             }
             const int arow = lane & 15, akoff = 16 * (lane >> 4);
+            if (th.w) {
+                // Compact tile: the B operand of lane (output n, group kg) for
+                // K step ks is block base + g - g0 of the lane holding it
+                // (ds_bpermute), zeros outside g0 .. g0 + len - 1; one plane
+                // at a time, so only 4 operand registers are live.
 #pragma unroll 1
-            for (int ks = 0; ks < th.y; ++ks) {
-                i32x4 bq[3];
-#pragma unroll
-                for (int p = 0; p < 3; ++p) bq[p] = __builtin_bit_cast(i32x4, bn[p]);
-                if (ks + 1 < th.y) {
+                for (int ks = 0; ks < th.y; ++ks) {
+                    const int rel = 4 * ks + (lane >> 4) - (meta & 0xFF);
+                    const bool ok = (unsigned)rel < (unsigned)((meta >> 8) & 0xFF);
+                    const int src = ((meta >> 16) + rel) << 2;
+                    const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
 #pragma unroll
                     for (int p = 0; p < 3; ++p) {
-#if defined(IPP_DIAG) && defined(IPP_DIAG_TAPHALF)
-                        if (ks + 1 < 2) continue;  // diagnostic (wrong output): K step 1 reuses step 0's taps
-#endif
-                        bn[p] = ld_tap(tblk_d, IPP_TAP_INDEX(th.z + lane + ((ks + 1) * 3 + p) * 64));
+                        const uint32_t w[4] = {bn[p].x, bn[p].y, bn[p].z, bn[p].w};
+                        i32x4 bq;
+#pragma unroll
+                        for (int d = 0; d < 4; ++d) {
+                            const int v = __builtin_amdgcn_ds_bpermute(src, (int)w[d]);
+                            bq[d] = ok ? v : 0;
+                        }
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const i32x4 av = *reinterpret_cast<const i32x4*>(&win[c][arow][pos]);
+                            acc[c][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bq, acc[c][p], 0, 0, 0);
+                        }
                     }
                 }
-                const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
+            } else {
+                // Dense tile (nK = 1, identity axes, or more than 64 nonzero
+                // groups): each K step's blocks loaded in turn.
+#pragma unroll 1
+                for (int ks = 0; ks < th.y; ++ks) {
+                    if (ks > 0) {
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const i32x4 a = *reinterpret_cast<const i32x4*>(&win[c][arow][pos]);
+                        for (int p = 0; p < 3; ++p) {
+#if defined(IPP_DIAG) && defined(IPP_DIAG_TAPHALF)
+                            if (ks < 2) continue;  // diagnostic (wrong output): K step 1 reuses step 0's taps
+#endif
+                            bn[p] = ld_tap(tblk_d, IPP_TAP_INDEX(th.z + lane + (ks * 3 + p) * 64));
+                        }
+                    }
+                    const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
 #pragma unroll
-                    for (int p = 0; p < 3; ++p)
-                        acc[c][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[p], acc[c][p], 0, 0, 0);
+                    for (int c = 0; c < 4; ++c) {
+                        const i32x4 av = *reinterpret_cast<const i32x4*>(&win[c][arow][pos]);
+#pragma unroll
+                        for (int p = 0; p < 3; ++p)
+                            acc[c][p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, __builtin_bit_cast(i32x4, bn[p]),
+                                                                            acc[c][p], 0, 0, 0);
+                    }
                 }
             }
             const int xo = 16 * t + (lane & 15);
@@ -500,7 +540,11 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                         const int32_t ss = acc[c][0][rr] + (acc[c][1][rr] << 8) + (acc[c][2][rr] << 16);
                         outc[c] |= clip8(ss) << (8 * rr);
                     }
-                const int grp = (row0 >> 2) + (lane >> 4);
+                // (an opaque lane copy: hoisted out of the chunk loop, this
+                // 64-bit row address was live through phase 1 and spilled)
+                int ln = lane;
+                asm volatile("" : "+v"(ln));
+                const int grp = (row0 >> 2) + (ln >> 4);
                 uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
                 const uint32_t w[4] = {outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
                                        outc[3] ^ 0x80808080u};
@@ -692,10 +736,11 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
         hpass2_body<NR, ZONES, CN, false>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
 }
 
-// 4 waves per SIMD (≤ 128 VGPRs); the > 8-range zone forms get 3 (they spill
-// at 128, and nothing may spill between an asm gather and its wait).
+// 4 waves per SIMD (≤ 128 VGPRs); the zone forms get 3 (their per-lane zone
+// bounds spill at 128, and nothing may spill between an asm gather and its
+// wait).
 template <int NR, bool ZONES, int CN>
-__global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES && NR > 8 ? 3 : 4)))
+__global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES ? 3 : 4)))
 k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
               const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp, const uint8_t* __restrict__ bg,
               uint8_t* __restrict__ dst, int cpi) {

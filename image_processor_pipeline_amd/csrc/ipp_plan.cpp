@@ -562,7 +562,7 @@ extern "C" int ipp_plan_pipe_batch(const ipp_pipe_plan_cfg* cfg, ipp_pipe_item* 
         const int32_t nkb_h = ipp_plan_mfma_nk_bound(rw, nw_, ks_h);
         const int32_t nkb_v = ipp_plan_mfma_nk_bound(rh, nh_, ks_v);
         if (!id_h && 64 * (int64_t)nkb_h > ring) return fail(start + i, E_RING);
-        ah = {rw, nw_, id_h ? 1 : 0, 0, 0, nkb_h, 0, (nw_ + 15) / 16, coef_words};
+        ah = {rw, nw_, id_h ? 1 : 0, 0, 0, nkb_h, 1, (nw_ + 15) / 16, coef_words};  // compact H tiles
         coef_words += (ipp_plan_mfma_size(rw, nw_, ks_h) + 3) / 4 * 4;
         const int32_t phase = it.y % 16;
         av = {rh, nh_, id_v ? 1 : 0, (!id_h && !id_v) ? y0 : 0, phase, nkb_v, 0, (nh_ + phase + 15) / 16, coef_words};

@@ -141,7 +141,29 @@ __global__ __launch_bounds__(256) void k_plan_taps(const ipp_tap_axis* __restric
             nK = a.nkb;
         }
         const int64_t boff = (int64_t)t * a.nkb * 192;
-        if (lane == 0) *reinterpret_cast<int4*>(hdr + 4 * t) = make_int4(K0, nK, (int)boff, 0);
+        // Compact layout (ipp.h, ipp_plan_mfma_tile): the 16 outputs' nonzero
+        // 16-column groups g0 .. g0 + len - 1, packed at base = the sum of the
+        // earlier outputs' len.
+        const bool cval = valid && cnt > 0;
+        const int g0 = cval ? (xs - K0) >> 4 : 0;
+        const int glen = cval ? ((xs + cnt - 1 - K0) >> 4) - g0 + 1 : 0;
+        int gbase = 0, nb = 0;
+        for (int c = 0; c < 16; ++c) {
+            const int lc = __shfl(glen, c);
+            gbase += c < col ? lc : 0;
+            nb += lc;
+        }
+        const bool compact = a.compact && !a.identity && nK >= 2 && nb <= 64;  // wave-uniform
+        if (lane == 0) *reinterpret_cast<int4*>(hdr + 4 * t) = make_int4(K0, nK, (int)boff, compact ? 1 : 0);
+        if (compact) {
+            // meta, the zero blocks past nb, and the zero tail of the tile's area
+            if (seg == 0) reinterpret_cast<int32_t*>(blk + boff)[col] = g0 | glen << 8 | gbase << 16;
+            if (lane >= nb) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) blk[boff + 4 + p * 64 + lane] = make_uint4(0u, 0u, 0u, 0u);
+            }
+            for (int u = 196 + lane; u < nK * 192; u += 64) blk[boff + u] = make_uint4(0u, 0u, 0u, 0u);
+        }
 
         // ---- filter weights of the tile, all lanes busy --------------------
         double ww = 0.0;
@@ -215,9 +237,19 @@ __global__ __launch_bounds__(256) void k_plan_taps(const ipp_tap_axis* __restric
                     }
                 }
             }
+            if (compact) {
+                const int g = 4 * s + seg;
+                if (cval && g >= g0 && g < g0 + glen) {
+                    const int i = gbase + g - g0;
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
-                blk[boff + (int64_t)(s * 3 + p) * 64 + lane] = make_uint4(P[p][0], P[p][1], P[p][2], P[p][3]);
+                    for (int p = 0; p < 3; ++p)
+                        blk[boff + 4 + p * 64 + i] = make_uint4(P[p][0], P[p][1], P[p][2], P[p][3]);
+                }
+            } else {
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    blk[boff + (int64_t)(s * 3 + p) * 64 + lane] = make_uint4(P[p][0], P[p][1], P[p][2], P[p][3]);
+            }
         }
         sum += __shfl_xor((long long)sum, 16);
         sum += __shfl_xor((long long)sum, 32);

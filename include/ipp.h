@@ -378,7 +378,8 @@ typedef struct ipp_tap_axis {
     int32_t shift;        /* subtracted from every xmin (V axis: ybox_first)  */
     int32_t phase;        /* tile phase (V axis: y mod 16)                    */
     int32_t nkb;          /* ipp_plan_mfma_nk_bound: K-step slots per tile     */
-    int32_t tile0;        /* unused (0)                                       */
+    int32_t compact;      /* 1: tiles may use the compact block layout (H
+                             axis of the pipe, see ipp_plan_mfma_tile)         */
     int32_t n_tiles;      /* (out_size + phase + 15) / 16                     */
     int64_t coef_off;     /* int32 index of the axis block in coefs           */
 } ipp_tap_axis;
@@ -420,7 +421,16 @@ int64_t ipp_pipe_taps_scratch_bytes(int32_t n_axes);
 int ipp_pipe_plan_taps(const ipp_tap_axis* axes, int32_t n_axes, int32_t* coefs, void* scratch,
                        int64_t* stats, void* stream);
 /* Host restatement of one tile of that format (Resample.c taps, libm sin):
- * hdr[4], bias[16], blocks (nK·3072 bytes, ≤ blocks_cap). */
+ * hdr[4], bias[16], blocks (nK·3072 bytes, ≤ blocks_cap).
+ * Compact layout (axis->compact, nK >= 2 and at most 64 nonzero 16-column
+ * groups over the tile's 16 outputs; hdr[3] = 1): bytes 0..63 hold
+ * meta[16], meta[n] = g0 | len << 8 | base << 16 (output n's taps lie in the
+ * 16-column groups g0 .. g0 + len - 1 counted from K0; base = the sum of len
+ * over the outputs before n); plane p's group block i (16 signed bytes) sits
+ * at byte 64 + (64 p + i)·16, block base + j holding output n's group g0 + j;
+ * everything else is zero.  The H pass loads one block per lane and plane and
+ * builds each K step's B operand by ds_bpermute (ipp_pipe.hip), 3 loads per
+ * tile instead of 3·nK. */
 int ipp_plan_mfma_tile(const ipp_tap_axis* axis, int32_t t, int32_t hdr[4], int32_t bias[16],
                        uint8_t* blocks, int64_t blocks_cap);
 /* Pieces of ipp_plan_pipe_batch exposed for the tests: the division-free
