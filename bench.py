@@ -69,6 +69,8 @@ def parse(argv=None):
                          "beside it")
     ap.add_argument("--stream-default-priority", action="store_true",
                     help="--stream: launch the pipe on the default-priority stream (not a high-priority one)")
+    ap.add_argument("--stream-lookahead", type=int, default=2,
+                    help="--stream: batches planned ahead of the running one (worker threads, side streams)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: CPU rehearsal of the N-rank path (tests)")
     ap.add_argument("--dump-digests", default=None,
@@ -423,7 +425,8 @@ def main(argv=None):
         # planned on a worker thread (host planner + device taps on a side
         # stream) while batch k-1 runs.  The clock starts with the pipeline
         # primed and stops when the last batch has finished.
-        ps = fused.PipeStream(dev, plan_batch, priority=not args.stream_default_priority)
+        ps = fused.PipeStream(dev, plan_batch, priority=not args.stream_default_priority,
+                              lookahead=args.stream_lookahead)
         clock = {}
 
         def mark():
@@ -444,7 +447,8 @@ def main(argv=None):
                       "kernel_ms": round(float(np.mean(kms)), 4),
                       "plan_host_ms": round(float(np.mean([t[0] for t in tim])), 2),
                       "taps_device_ms": round(float(np.mean([t[1] for t in tim])), 2),
-                      "taps_host_tiles": round(float(np.mean([t[2] for t in tim])), 1)}
+                      "taps_host_tiles": round(float(np.mean([t[2] for t in tim])), 1),
+                      "lookahead": ps.lookahead}
 
     if args.dump_digests:
         mine = outputs()

@@ -14,12 +14,14 @@
 // tap whose value lies within 2^-22 of an integer is listed and rebuilt on the
 // host with libm (ipp_plan_mfma_tile), so the result is bit-exact.
 //
-// One block per axis, one wave per 16-output tile.  A wave first evaluates
-// the filter for all (output, tap) pairs of its tile across its 64 lanes
-// (weights cached in LDS), sums each output's weights in Pillow's order on
-// one lane, then lane (seg, col) builds the 16-byte chunks of output col at
-// K offsets 16·seg + 64·s — exactly one lane owns each chunk, so every block
-// is written once, with full 16-byte stores and no memset.
+// One block per axis, one wave per 16-output tile.  Lane (seg, col) owns taps
+// q = seg + 4i of output col: it evaluates their weights into an LDS cache,
+// one lane per output sums them in Pillow's order, then every
+// lane quantises its own taps and writes their three byte planes into an LDS
+// staging area laid out as the tile's blocks (dense: a window of K steps at a
+// time; compact: the whole 196-uint4 tile), which the wave stores with full
+// 16-byte coalesced stores.  The VALU work is per (output, tap) pair, not per
+// (output, K position): ~5x fewer lanes idle than a chunk-per-lane build.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -34,6 +36,10 @@ namespace {
 
 constexpr int TAP_WAVES = 4;
 constexpr int TAP_CACHE = 64;       // cached weights per output (more: recomputed)
+constexpr int TAP_NI = TAP_CACHE / 4;  // weights per lane in registers (4 lanes per output)
+constexpr int TAP_STAGE_U4 = 16 * TAP_CACHE * 8 / 16;  // per wave: the weight cache = the staging area
+constexpr int TAP_STAGE_K = TAP_STAGE_U4 / 192;         // dense K steps per staging window
+static_assert(TAP_STAGE_U4 >= 196 && TAP_STAGE_K >= 1, "staging area holds a compact tile");
 constexpr int TAP_FLAG_CAP = 1 << 16;
 constexpr double TAP_NEAR = 1.0 / 4194304.0;  // 2^-22
 
@@ -93,15 +99,33 @@ inline __device__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(256) void k_plan_taps(const ipp_tap_axis* __restrict__ axes,
-                                                   int32_t* __restrict__ coefs, int32_t* __restrict__ ctl,
-                                                   int2* __restrict__ flags) {
-    __shared__ double wcache[TAP_WAVES][16][TAP_CACHE];
-    __shared__ double s_ww[TAP_WAVES][16];
-    __shared__ double s_center[TAP_WAVES][16];
-    __shared__ int s_xmin[TAP_WAVES][16];
-    __shared__ int s_pre[TAP_WAVES][16];
-    __shared__ int s_cnt[TAP_WAVES][16];
+// Pillow's 8bpc normalisation of one weight (Resample.c normalize_coeffs_8bpc,
+// PRECISION_BITS 22): k = trunc(v·2^22 ± 0.5), v = w / ww; `near` when the
+// pre-truncation value is within 2^-22 of an integer (the host rebuilds that
+// tile with libm).
+__device__ inline int32_t d_quant(double w, double rww, bool& near) {
+    const double v = w * rww;
+    const double x = v < 0 ? -0.5 + v * 4194304.0 : 0.5 + v * 4194304.0;
+    near |= fabs(x - rint(x)) < TAP_NEAR;
+    return (int32_t)x;
+}
+
+// Byte address, in the wave's staging area, of plane p of tap K index kidx
+// (relative to the tile's K0) of output col.  Dense: chunk (s, p, seg, col)
+// at uint4 (3s + p)·64 + 16·seg + col of the window that starts at K step s0.
+// Compact: block gbase + (kidx >> 4) - g0 of plane p, after the 4 meta uint4.
+__device__ inline int stage_byte(bool compact, int kidx, int p, int col, int s0, int g0, int gbase) {
+    const int u = compact ? 4 + p * 64 + gbase + (kidx >> 4) - g0
+                          : ((((kidx >> 6) - s0) * 3 + p) * 64 + ((kidx >> 4) & 3) * 16 + col);
+    return 16 * u + (kidx & 15);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_plan_taps(
+    const ipp_tap_axis* __restrict__ axes, int32_t* __restrict__ coefs, int32_t* __restrict__ ctl,
+    int2* __restrict__ flags) {
+    // per wave: the weight cache of the running sums, then (same bytes) the
+    // staging area the tile's blocks are assembled in
+    __shared__ uint4 s_wave[TAP_WAVES][TAP_STAGE_U4];
     const ipp_tap_axis a = axes[blockIdx.x];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, col = lane & 15, seg = lane >> 4;
     const double scale = (double)((float)a.in_size) / a.out_size;
@@ -110,7 +134,9 @@ __global__ __launch_bounds__(256) void k_plan_taps(const ipp_tap_axis* __restric
     int32_t* hdr = coefs + a.coef_off;
     int32_t* bias = hdr + 4 * (int64_t)a.n_tiles;
     uint4* blk = reinterpret_cast<uint4*>(hdr + 20 * (int64_t)a.n_tiles);
-    double* wc = &wcache[wave][0][0];
+    double* wc = reinterpret_cast<double*>(&s_wave[wave][0]);    // [16][TAP_CACHE]
+    uint8_t* stage = reinterpret_cast<uint8_t*>(&s_wave[wave][0]);
+    uint4* stage4 = &s_wave[wave][0];
 
     for (int t = wave; t < a.n_tiles; t += TAP_WAVES) {
         const int o0 = 16 * t - a.phase, o = o0 + col;
@@ -133,13 +159,17 @@ __global__ __launch_bounds__(256) void k_plan_taps(const ipp_tap_axis* __restric
         }
         const int xs = xmin - a.shift;
         const int K0 = __shfl(xs, oa - o0) & ~15;
-        int end = valid ? xs + cnt : K0;
-        for (int m = 32; m >= 1; m >>= 1) end = max(end, __shfl_xor(end, m));
+        int end = valid ? xs + cnt : K0, maxcnt = cnt;
+        for (int m = 32; m >= 1; m >>= 1) {
+            end = max(end, __shfl_xor(end, m));
+            maxcnt = max(maxcnt, __shfl_xor(maxcnt, m));
+        }
         int nK = (max(end, K0) - K0 + 63) >> 6;
         if (nK > a.nkb) {  // the planner's bound was wrong: report, stay in bounds
             if (lane == 0) atomicOr(ctl + 1, 1);
             nK = a.nkb;
         }
+        const int niter = (maxcnt + 3) >> 2;   // lane (seg, col) holds taps q = seg + 4i of output col
         const int64_t boff = (int64_t)t * a.nkb * 192;
         // Compact layout (ipp.h, ipp_plan_mfma_tile): the 16 outputs' nonzero
         // 16-column groups g0 .. g0 + len - 1, packed at base = the sum of the
@@ -155,102 +185,101 @@ __global__ __launch_bounds__(256) void k_plan_taps(const ipp_tap_axis* __restric
         }
         const bool compact = a.compact && !a.identity && nK >= 2 && nb <= 64;  // wave-uniform
         if (lane == 0) *reinterpret_cast<int4*>(hdr + 4 * t) = make_int4(K0, nK, (int)boff, compact ? 1 : 0);
-        if (compact) {
-            // meta, the zero blocks past nb, and the zero tail of the tile's area
-            if (seg == 0) reinterpret_cast<int32_t*>(blk + boff)[col] = g0 | glen << 8 | gbase << 16;
-            if (lane >= nb) {
-#pragma unroll
-                for (int p = 0; p < 3; ++p) blk[boff + 4 + p * 64 + lane] = make_uint4(0u, 0u, 0u, 0u);
-            }
-            for (int u = 196 + lane; u < nK * 192; u += 64) blk[boff + u] = make_uint4(0u, 0u, 0u, 0u);
-        }
 
-        // ---- filter weights of the tile, all lanes busy --------------------
+        // ---- filter weights: lane (seg, col) evaluates taps seg + 4i --------
         double ww = 0.0;
         if (!a.identity) {
-            if (seg == 0) {
-                s_center[wave][col] = center;
-                s_xmin[wave][col] = xmin;
-            }
-            int pre = 0, total = 0;  // prefix of cached tap counts over columns
-            for (int c = 0; c < 16; ++c) {
-                const int nc = min(__shfl(cnt, c), TAP_CACHE);
-                if (c < col) pre += nc;
-                total += nc;
-            }
-            if (seg == 0) {
-                s_pre[wave][col] = pre;
-                s_cnt[wave][col] = min(cnt, TAP_CACHE);
-            }
-            wave_sync();
-            for (int p = lane; p < total; p += 64) {
-                int c = 0, base = 0;
-                for (int k = 0; k < 16; ++k) {  // column of pair p
-                    const int bk = s_pre[wave][k];
-                    if (bk <= p && s_cnt[wave][k] > 0) {
-                        c = k;
-                        base = bk;
-                    }
-                }
-                const int q = p - base;
-                wc[c * TAP_CACHE + q] = d_weight(q, s_xmin[wave][c], s_center[wave][c], ss);
+            for (int i = 0; i < min(niter, TAP_NI); ++i) {
+                const int q = 4 * i + seg;
+                if (q < cnt) wc[col * TAP_CACHE + q] = d_weight(q, xmin, center, ss);
             }
             wave_sync();
             if (seg == 0 && valid) {  // Pillow's running sum, in tap order
                 for (int q = 0; q < cnt; ++q)
                     ww += q < TAP_CACHE ? wc[col * TAP_CACHE + q] : d_weight(q, xmin, center, ss);
-                s_ww[wave][col] = ww;
             }
-            wave_sync();
-            ww = s_ww[wave][col];
+            ww = __shfl(ww, col);
         }
 
-        // ---- chunks of output col at K offset 64s + 16seg ------------------
+        // ---- quantised taps: per lane its K indices and packed byte planes --
+        const double rww = ww != 0.0 ? 1.0 / ww : 1.0;  // (a few ulps from v / ww: see d_sinpi)
+        int32_t kx[TAP_NI];                     // K index rel. K0 (-1: none)
+        uint32_t pb[TAP_NI];                    // balanced signed bytes of the three planes
         int64_t sum = 0;
         bool near = false;
-        const double rww = ww != 0.0 ? 1.0 / ww : 1.0;  // (a few ulps from v / ww: see d_sinpi)
-        for (int s = 0; s < nK; ++s) {
-            uint32_t P[3][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-            const int qb = K0 + 64 * s + 16 * seg - xs;
-            if (valid && qb < cnt && qb + 16 > 0) {
+        auto pack = [](int32_t k) {
+            uint32_t b = 0;
+            int32_t r = k;
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int q = qb + j;
-                    if (q < 0 || q >= cnt) continue;
-                    int32_t k;
-                    if (a.identity) {
-                        k = 1 << 22;
-                    } else {
-                        double v = q < TAP_CACHE ? wc[col * TAP_CACHE + q] : d_weight(q, xmin, center, ss);
-                        v = v * rww;
-                        const double x = v < 0 ? -0.5 + v * 4194304.0 : 0.5 + v * 4194304.0;
-                        k = (int32_t)x;
-                        near |= fabs(x - rint(x)) < TAP_NEAR;
-                    }
-                    sum += k;
-                    int32_t r = k;
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) {  // balanced signed bytes
-                        const int32_t lo = ((r + 128) & 255) - 128;
-                        P[p][j >> 2] |= (uint32_t)(uint8_t)lo << (8 * (j & 3));
-                        r = (r - lo) >> 8;
-                    }
-                }
+            for (int p = 0; p < 3; ++p) {
+                const int32_t lo = ((r + 128) & 255) - 128;
+                b |= (uint32_t)(lo & 255) << (8 * p);
+                r = (r - lo) >> 8;
             }
-            if (compact) {
-                const int g = 4 * s + seg;
-                if (cval && g >= g0 && g < g0 + glen) {
-                    const int i = gbase + g - g0;
+            return b;
+        };
 #pragma unroll
-                    for (int p = 0; p < 3; ++p)
-                        blk[boff + 4 + p * 64 + i] = make_uint4(P[p][0], P[p][1], P[p][2], P[p][3]);
-                }
-            } else {
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    blk[boff + (int64_t)(s * 3 + p) * 64 + lane] = make_uint4(P[p][0], P[p][1], P[p][2], P[p][3]);
+        for (int i = 0; i < TAP_NI; ++i) {
+            const int q = 4 * i + seg;
+            kx[i] = -1;
+            pb[i] = 0;
+            if (i < niter && q < cnt) {
+                const int32_t k = a.identity ? (1 << 22) : d_quant(wc[col * TAP_CACHE + q], rww, near);
+                sum += k;
+                kx[i] = xs + q - K0;
+                pb[i] = pack(k);
             }
         }
+        for (int i = TAP_NI; i < niter; ++i) {  // beyond the register set (scale > 10.5): recomputed
+            const int q = 4 * i + seg;
+            if (q < cnt) sum += d_quant(d_weight(q, xmin, center, ss), rww, near);
+        }
+        wave_sync();                            // the staging area reuses the cache
+
+        // ---- assemble the blocks in LDS, window by window, then store ------
+        const int sw = compact ? nK : TAP_STAGE_K;
+        for (int s0 = 0; s0 < nK; s0 += sw) {
+            const int nu = compact ? 196 : 192 * min(sw, nK - s0);
+            for (int u = lane; u < nu; u += 64) stage4[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (compact && seg == 0) reinterpret_cast<int32_t*>(stage)[col] = g0 | glen << 8 | gbase << 16;
+            wave_sync();
+            auto put = [&](int kidx, uint32_t b) {
+                asm volatile("" : "+v"(kidx));  // per window: nothing of it hoisted out of the window loop
+                if (kidx < 0 || (!compact && ((kidx >> 6) < s0 || (kidx >> 6) >= s0 + sw))) return;
+                // planes 64 uint4 (1 KB) apart in both layouts
+                uint8_t* d = stage + stage_byte(compact, kidx, 0, col, s0, g0, gbase);
+                d[0] = (uint8_t)b;
+                d[1024] = (uint8_t)(b >> 8);
+                d[2048] = (uint8_t)(b >> 16);
+            };
+#pragma unroll
+            for (int i = 0; i < TAP_NI; ++i)
+                if (i < niter) put(kx[i], pb[i]);
+            wave_sync();
+            for (int u = lane; u < nu; u += 64) blk[boff + 192 * (int64_t)s0 + u] = stage4[u];
+            wave_sync();                        // the next window / tile rewrites the area
+        }
+        if (niter > TAP_NI) {
+            // taps past the register set (scale > 10.5, never a compact tile):
+            // recomputed and stored as bytes over the zeros just written
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            uint8_t* tile = reinterpret_cast<uint8_t*>(blk + boff);
+            for (int i = TAP_NI; i < niter; ++i) {
+                const int q = 4 * i + seg;
+                bool nr = false;
+                if (q >= cnt) continue;
+                const int kidx = xs + q - K0;
+                if ((kidx >> 6) >= nK) continue;
+                const uint32_t b = pack(d_quant(d_weight(q, xmin, center, ss), rww, nr));
+                uint8_t* d = tile + stage_byte(compact, kidx, 0, col, 0, g0, gbase);
+                d[0] = (uint8_t)b;
+                d[1024] = (uint8_t)(b >> 8);
+                d[2048] = (uint8_t)(b >> 16);
+            }
+        }
+        if (compact)  // the zero tail of the tile's area
+            for (int u = 196 + lane; u < nK * 192; u += 64) blk[boff + u] = make_uint4(0u, 0u, 0u, 0u);
+
         sum += __shfl_xor((long long)sum, 16);
         sum += __shfl_xor((long long)sum, 32);
         if (seg == 0) bias[16 * t + col] = valid ? (int32_t)((1 << 21) + 128 * sum) : 0;
@@ -258,7 +287,6 @@ __global__ __launch_bounds__(256) void k_plan_taps(const ipp_tap_axis* __restric
             const int idx = atomicAdd(ctl, 1);
             if (idx < TAP_FLAG_CAP) flags[idx] = make_int2((int)blockIdx.x, t);
         }
-        wave_sync();  // the next tile reuses the weight cache
     }
 }
 

@@ -340,24 +340,31 @@ class PipeRunner:
 
 class PipeStream:
     """Streaming form of PipeRunner (bench.py --stream): every batch has its
-    own plan, built while the previous batch runs.  A worker thread runs
-    batch k+1's host plan (ipp_plan_pipe_batch; ctypes drops the GIL) and
-    its device taps (ipp_pipe_plan_taps on a side stream) while batch k's
-    two launches run on the pipe stream.  Device buffers live in
-    `slots` sets that alternate; a set is refilled only after the batch that
-    last used it has completed (its HIP event)."""
+    own plan, built while earlier batches run.  Worker threads run the host
+    plans (ipp_plan_pipe_batch; ctypes drops the GIL) and device taps
+    (ipp_pipe_plan_taps, one side stream per slot) of batches k+1 ..
+    k+lookahead while batch k's two launches run on the pipe stream.  Device
+    buffers live in `slots` (≥ lookahead + 1) sets used in turn; a set is
+    refilled only after the batch that last used it has completed (its HIP
+    event)."""
 
-    def __init__(self, device, plan_fn, slots: int = 2, priority: bool = True):
+    def __init__(self, device, plan_fn, slots: int = 3, priority: bool = True, lookahead: int = 2):
         self.device = torch.device(device)
         self.plan_fn = plan_fn                  # batch index -> PipePlan
         self.lib = N.load()
-        self.side = torch.cuda.Stream(self.device)
+        # batches k+1 .. k+lookahead are being planned while batch k runs
+        # (each on its own worker thread and side stream): the tap planner of
+        # one batch then has `lookahead` batch times to get its share of the
+        # GPU beside the pipe
+        self.lookahead = max(1, int(lookahead))
+        slots = max(slots, self.lookahead + 1)
         # The pipe launches go to a high-priority stream (the hardware queue
         # dispatches its blocks first): the tap planner of the next batch, on
         # the default-priority side stream, then fills the CU slots the pipe
         # leaves free instead of displacing H-pass blocks.
         self.main = torch.cuda.Stream(self.device, priority=-1) if priority else None
-        self.slots = [{"done": torch.cuda.Event(), "bufs": {}} for _ in range(max(2, slots))]
+        self.slots = [{"done": torch.cuda.Event(), "bufs": {}, "side": torch.cuda.Stream(self.device)}
+                      for _ in range(max(2, slots))]
         self.timing: List[Tuple[float, float, int]] = []   # per batch: host plan ms, taps ms, host tiles
         self.events: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []
 
@@ -379,11 +386,12 @@ class PipeStream:
                 "tmp": self._buf(slot, "tmp", plan.tmp_bytes),
                 "scratch": self._buf(slot, "scratch", self.lib.ipp_pipe_taps_scratch_bytes(len(plan.axes)))}
         stats = np.zeros(2, np.int64)
-        with torch.cuda.stream(self.side):
+        side = slot["side"]
+        with torch.cuda.stream(side):
             bufs["descs"][:plan.descs.nbytes].copy_(torch.from_numpy(plan.descs.view(np.uint8)))
             N.check(self.lib.ipp_pipe_plan_taps(N.np_ptr(plan.axes), len(plan.axes), bufs["coefs"].data_ptr(),
                                                 bufs["scratch"].data_ptr(), N.np_ptr(stats),
-                                                self.side.cuda_stream), "ipp_pipe_plan_taps")
+                                                side.cuda_stream), "ipp_pipe_plan_taps")
         if stats[1]:
             raise N.NativeError(f"ipp_pipe_plan_taps: device status {int(stats[1])}")
         t2 = time.perf_counter()
@@ -393,21 +401,24 @@ class PipeStream:
             record: bool = False) -> None:
         """Run batches 0 .. n_batches-1 (plan_fn(k) plans batch k).  `mark`
         (optional callable) is called right before batch `mark.at` is
-        launched, with the pipeline primed (its plan ready, the next one not
-        yet started) — bench.py starts its clock there."""
+        launched, with the pipeline primed (its plan ready, the following
+        lookahead-1 plans in flight) — bench.py starts its clock there."""
         from concurrent.futures import ThreadPoolExecutor
         main = self.main if self.main is not None else torch.cuda.current_stream(self.device)
         if self.main is not None:
             self.main.wait_stream(torch.cuda.current_stream(self.device))  # inputs written on the caller's stream
-        with ThreadPoolExecutor(1) as ex:
-            fut = ex.submit(self._prepare, 0, self.slots[0])
+        L, ns = self.lookahead, len(self.slots)
+        with ThreadPoolExecutor(L) as ex:
+            futs = {j: ex.submit(self._prepare, j, self.slots[j % ns]) for j in range(min(L, n_batches))}
             for k in range(n_batches):
-                plan, b, tm = fut.result()
+                plan, b, tm = futs.pop(k).result()
                 if mark is not None and k == mark.at:
                     mark()
-                slot = self.slots[k % len(self.slots)]
-                if k + 1 < n_batches:
-                    fut = ex.submit(self._prepare, k + 1, self.slots[(k + 1) % len(self.slots)])
+                slot = self.slots[k % ns]
+                if k + L < n_batches:
+                    # its slot was last used by batch k + L - ns <= k - 1, whose
+                    # completion event is already recorded
+                    futs[k + L] = ex.submit(self._prepare, k + L, self.slots[(k + L) % ns])
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if record else None
                 if ev:
                     ev[0].record(main)

@@ -45,6 +45,9 @@ def _check_axes(plan, coefs, axes_idx):
     ((480, 640), 25, (720, 1280), 7, F.PipeConfig(margins=(0, 0, 0, 0), scale_min=0.4, scale_max=0.9), 3),
     # upscales (ratio > source) and near-identity axes
     ((200, 160), 30, (1024, 1024), 2, F.PipeConfig(margins=(0, 0, 0, 0), scale_min=0.5, scale_max=0.9), 11),
+    # long filters: ratios 11-19, up to ~117 taps per output (past the
+    # planner's 64 register-held taps), 7 K steps (several staging windows)
+    ((1024, 1024), 20, (640, 640), 3, F.PipeConfig(scale_min=0.1, scale_max=0.15), 5),
 ])
 def test_device_taps_equal_host_taps(case):
     if not torch.cuda.is_available():
