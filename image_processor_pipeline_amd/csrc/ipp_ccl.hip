@@ -1012,7 +1012,8 @@ k_ccl_crop_stream(const uint8_t* __restrict__ img, const ipp_image_desc* __restr
     auto put = [&](const uint32_t (&o)[4], int n, uint32_t* q) {
         if (n == 4 && ((reinterpret_cast<uintptr_t>(q) & 15u) == 0u)) {
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            *reinterpret_cast<u32x4*>(q) = u32x4{o[0], o[1], o[2], o[3]};
+            // streaming store (-0.7 % against a plain one)
+            __builtin_nontemporal_store(u32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<u32x4*>(q));
         } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i)

@@ -103,7 +103,10 @@ __device__ __forceinline__ void rotate_tiles(const uint8_t* __restrict__ src, ui
         if (sy >= d.out_h || sx0 >= d.out_w) continue;
         uint8_t* o = dst + d.dst_off + (int64_t)sy * d.dst_pitch + 4 * sx0;
         if (sx0 + 4 <= d.out_w && ((reinterpret_cast<uintptr_t>(o) & 15u) == 0)) {
-            *reinterpret_cast<uint4*>(o) = px;
+            // streaming (nontemporal) store: the output is not re-read here, and
+            // plain stores that allocate in L2 cost 25 % (3.55 vs 2.84 ms)
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(v4u{px.x, px.y, px.z, px.w}, reinterpret_cast<v4u*>(o));
         } else {
             const uint32_t pv[4] = {px.x, px.y, px.z, px.w};
             for (int k = 0; k < 4; ++k)
