@@ -575,6 +575,25 @@ __device__ __forceinline__ void paste_bands(const ipp_paste_desc& p, int& vb0, i
     vb1 = max(vb1, vb0);
 }
 
+// Column split of the band rows [vb0, vb1): on dense, 16-B aligned images
+// whose width is a multiple of 16, the H pass's copy blocks also write the
+// band rows' 16-pixel groups outside [gx0, gx1) (the groups the overlay
+// touches) and the V pass visits only [gx0, gx1).  Both kernels decide it
+// with this one predicate (ipp_plan.cpp counts the bytes the same way).
+#ifndef IPP_BAND_SPLIT
+#define IPP_BAND_SPLIT 1  // (0: experiment builds, the V pass copies whole band rows)
+#endif
+__device__ __forceinline__ bool band_cols_split(const ipp_paste_desc& p, const uint8_t* bg, const uint8_t* dst,
+                                                int& gx0, int& gx1) {
+    const int rb = 3 * p.bg_w;
+    gx0 = max(p.x, 0) >> 4;
+    gx1 = min((p.x + p.ov_w + 15) >> 4, p.bg_w >> 4);
+    const int64_t lr = 3 * (p.bg_w >> 4);  // ≥ the split's vectors per band row
+    return IPP_BAND_SPLIT && (p.bg_w & 15) == 0 && p.bg_pitch == rb && p.dst_pitch == rb && gx0 < gx1 &&
+           (int64_t)p.bg_h * lr * lr < (1ll << 32) &&  // (the H copy's umulhi division stays exact)
+           ((reinterpret_cast<uintptr_t>(bg + p.bg_off) | reinterpret_cast<uintptr_t>(dst + p.dst_off)) & 15u) == 0;
+}
+
 // 16-B vectors per thread in flight in the background copy (IPP_COPY_U
 // overrides it in experiment builds).  A copy block holds one of the CU's
 // four H-pass block slots for as long as it streams, so bytes in flight per
@@ -593,10 +612,25 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
     const bool flat = p.bg_pitch == rb && p.dst_pitch == rb && (rb & 15) == 0 &&
                       ((reinterpret_cast<uintptr_t>(sb) | reinterpret_cast<uintptr_t>(db)) & 15u) == 0;
     if (flat) {
-        // Two flat byte ranges [0, vb0·rb) and [vb1·rb, bg_h·rb) in 16-B vectors.
-        const int64_t n0 = (int64_t)vb0 * rb / 16, n1 = (int64_t)(p.bg_h - vb1) * rb / 16, V = n0 + n1;
+        // Two flat byte ranges [0, vb0·rb) and [vb1·rb, bg_h·rb) in 16-B
+        // vectors, then (column split) each band row's L vectors left of the
+        // overlay's groups and R right of them.
+        int gx0, gx1;
+        const bool split = band_cols_split(p, bg, dst, gx0, gx1);
+        const int L = split ? 3 * gx0 : 0, LR = split ? 3 * ((p.bg_w >> 4) - gx1) + L : 0;
+        const int rv = rb / 16, rgt = 3 * gx1 - L;       // vectors per row; right part's column shift
+        const uint32_t mag = LR > 0 ? (uint32_t)((0x100000000ull + LR - 1) / LR) : 0u;  // j / LR = umulhi(j, mag)
+        const int64_t n0 = (int64_t)vb0 * rb / 16, n1 = (int64_t)(p.bg_h - vb1) * rb / 16;
+        const int64_t n2 = (int64_t)(vb1 - vb0) * LR, V = n0 + n1 + n2;
         const int64_t a = V * share / nshare, e = V * (share + 1) / nshare;
         const int64_t skip = (int64_t)vb1 * rb / 16 - n0;  // vector index gap over the bands
+        auto vec_of = [&](int64_t i) -> int64_t {
+            if (i < n0) return i;
+            if (i < n0 + n1) return i + skip;
+            const uint32_t j = (uint32_t)(i - n0 - n1);   // j·LR < 2^32: umulhi exact
+            const uint32_t r = __umulhi(j, mag), c = j - r * (uint32_t)LR;
+            return (int64_t)(vb0 + (int)r) * rv + (int)c + ((int)c < L ? 0 : rgt);
+        };
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4* s4 = reinterpret_cast<const u32x4*>(sb);
         u32x4* d4 = reinterpret_cast<u32x4*>(db);
@@ -607,7 +641,7 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
             for (int j = 0; j < U; ++j) {
                 const int64_t i = i0 + NT * j;
                 if (i < e) {
-                    const int64_t k = i < n0 ? i : i + skip;
+                    const int64_t k = vec_of(i);
                     if (IPP_COPY_POL == 0) v[j] = s4[k];
                     else v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, (uint32_t)k * 16u, 0, IPP_COPY_POL));
                 }
@@ -615,7 +649,7 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
 #pragma unroll
             for (int j = 0; j < U; ++j) {
                 const int64_t i = i0 + NT * j;
-                if (i < e) __builtin_nontemporal_store(v[j], d4 + (i < n0 ? i : i + skip));
+                if (i < e) __builtin_nontemporal_store(v[j], d4 + vec_of(i));
             }
         }
         return;
@@ -864,12 +898,17 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
     const bool groups = (p.bg_w & 15) == 0 && ((p.bg_pitch | p.dst_pitch) & 15) == 0 &&
                         ((reinterpret_cast<uintptr_t>(bgb) | reinterpret_cast<uintptr_t>(dsb)) & 15u) == 0 &&
                         !(DBG & 1) && !(kVbX & 4);
-    const int G = p.bg_w >> 4, lg = 31 - __builtin_clz(max(G, 1));
+    // groups per row visited: all of them, or (column split) the overlay's
+    // [sx0, sx1) — the H pass's copy blocks wrote the rest of the band rows
+    int sx0, sx1;
+    const bool csplit = groups && band_cols_split(p, bg, dst, sx0, sx1);
+    const int gc0 = csplit ? sx0 : 0;
+    const int G = csplit ? sx1 - sx0 : p.bg_w >> 4, lg = 31 - __builtin_clz(max(G, 1));
     const bool pow2 = (G & (G - 1)) == 0;
     const int gtotal = nrows * G;
     auto gload = [&](int idx, uint4 (&v)[3]) {
         const int rr = pow2 ? idx >> lg : idx / G;
-        const int gi = idx - rr * G;
+        const int gi = gc0 + idx - rr * G;
         const uint4* sp = reinterpret_cast<const uint4*>(bgb + (int64_t)rr * p.bg_pitch) + 3 * gi;
 #pragma unroll
         for (int q = 0; q < 3; ++q) v[q] = sp[q];
@@ -999,7 +1038,7 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
             uint4 gnxt[3];
             if (IPP_VB_PF >= 1 && idx + 256 < gtotal) gload(idx + 256, gnxt);
             const int rr = pow2 ? idx >> lg : idx / G;
-            const int gi = idx - rr * G;
+            const int gi = gc0 + idx - rr * G;
             uint32_t w[12];
 #pragma unroll
             for (int q = 0; q < 3; ++q) {

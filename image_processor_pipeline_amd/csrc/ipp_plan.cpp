@@ -535,7 +535,7 @@ extern "C" int ipp_plan_pipe_batch(const ipp_pipe_plan_cfg* cfg, ipp_pipe_item* 
     }
 
     // ---- axes, descriptors, totals -----------------------------------------
-    int64_t coef_words = 0, tmp_off = 0, algo_h = 0, algo_v = 0, copy_rows = 0;
+    int64_t coef_words = 0, tmp_off = 0, algo_h = 0, algo_v = 0, copy_rows = 0, copy_band_bytes = 0;
     int32_t max_out_w = 1, max_rows = 1, max_ov_w = 1, max_ov_h = 1, max_tiles = 1;
     std::vector<ipp_pipe_desc> d(n);
     for (int32_t i = 0; i < n; ++i) {
@@ -637,6 +637,13 @@ extern "C" int ipp_plan_pipe_batch(const ipp_pipe_plan_cfg* cfg, ipp_pipe_item* 
         const int32_t vb0 = (it.y / 16) * 16;
         const int32_t vb1 = std::max(vb0, std::min(bh, (it.y + nh_ + 15) / 16 * 16));
         copy_rows += bh - (vb1 - vb0);
+        // the band rows' 16-pixel groups outside the overlay's, copied by the
+        // H pass too when ipp_pipe.hip's band_cols_split holds (dense rows;
+        // 16-B aligned images assumed)
+        const int32_t gx0 = std::max(it.x, 0) >> 4, gx1 = std::min((it.x + nw_ + 15) >> 4, bw >> 4);
+        const int64_t lr = 3 * (int64_t)(bw >> 4);
+        if ((bw & 15) == 0 && ((int64_t)3 * bh * bw) % 16 == 0 && gx0 < gx1 && (int64_t)bh * lr * lr < (1ll << 32))
+            copy_band_bytes += 2 * 48 * (int64_t)(vb1 - vb0) * ((bw >> 4) - (gx1 - gx0));
     }
     // processing order: items grouped by background (stable), see fused.py
     std::vector<int32_t> ord(n);
@@ -644,7 +651,7 @@ extern "C" int ipp_plan_pipe_batch(const ipp_pipe_plan_cfg* cfg, ipp_pipe_item* 
     std::stable_sort(ord.begin(), ord.end(),
                      [&](int32_t a, int32_t b) { return items[a].bg_index < items[b].bg_index; });
     for (int32_t i = 0; i < n; ++i) descs[i] = d[ord[i]];
-    const int64_t copy_bytes = 2 * 3 * (int64_t)bw * copy_rows;
+    const int64_t copy_bytes = 2 * 3 * (int64_t)bw * copy_rows + copy_band_bytes;
     totals[IPP_PT_COEF_WORDS] = coef_words;
     totals[IPP_PT_TMP_BYTES] = std::max<int64_t>(tmp_off, 256);
     totals[IPP_PT_MAX_OUT_W] = max_out_w;
