@@ -480,6 +480,16 @@ def main(argv=None):
     if ceiling:
         roofline["copy_ceiling"] = round(ceiling, 1)
         roofline["frac_of_copy_ceiling"] = round(achieved / ceiling, 4)
+    # The whole step against the same peak: every launch's algorithmic bytes
+    # over the driver-clocked step time, so moving work (or bytes) from one
+    # launch to another cannot move it; with pipe5 also the fixed fused lower
+    # bound (read the crop, read the background, write the composite).
+    step_gbps = step_algo / (ms_step * 1e-3) / 1e9
+    roofline["step"] = {"algo_bytes": int(step_algo), "ms": round(ms_step, 3), "achieved": round(step_gbps, 1),
+                        "frac": round(step_gbps / HBM_PEAK_GBPS, 4)}
+    if fused_bound is not None:
+        roofline["step"]["fused_bound_bytes"] = int(fused_bound)
+        roofline["step"]["fused_bound_frac"] = round(fused_bound / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
     result = {
         "metric": METRICS[args.workload],
         "value": round(value, 1),

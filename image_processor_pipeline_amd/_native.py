@@ -109,7 +109,7 @@ TAP_AXIS = np.dtype([
 # ipp_plan_pipe_batch totals[] slots (ipp.h IPP_PT_*)
 IPP_PLAN_TOTALS = 16
 PT = dict(coef_words=0, tmp_bytes=1, max_out_w=2, max_rows=3, max_ov_w=4, max_ov_h=5, algo_h=6, algo_v=7,
-          copy_bytes=8, max_tiles=9, err_item=10, err_code=11)
+          copy_bytes=8, max_tiles=9, err_item=10, err_code=11, copy_reads=12)
 
 # (symbol, restype, argtypes) — every entry point declared in include/ipp.h.
 _P = ctypes.c_void_p
@@ -147,6 +147,7 @@ SIGNATURES = {
     "ipp_plan_pipe_batch": (_I, [_P, _P, _P, _P, _P]),
     "ipp_pipe_taps_scratch_bytes": (_L, [_I]),
     "ipp_pipe_plan_taps": (_I, [_P, _I, _P, _P, _P, _P]),
+    "ipp_pipe_plan_taps_cap": (_I, [_P, _I, _P, _P, _P, _L, _P]),
     "ipp_plan_mfma_tile": (_I, [_P, _I, _P, _P, _P, _L]),
     "ipp_plan_opaque_bbox_fast": (_I, [_I, _I, _P, _I, _I, _P]),
     "ipp_plan_py_hypot": (_D, [_D, _D]),

@@ -37,23 +37,11 @@ constexpr int RING = 512;         // window ring: M columns x live at x & (RING 
 // 64 distinct banks per group, and the phase-1 ds_write_b32 rows pair up 2-way,
 // which a dword store absorbs (MI355X_MICROARCH.md §LDS).
 constexpr int WSTRIDE = 544;
-// ipp_pipe_hpass_bgcopy: background-copy blocks per item.  Diagnostic builds
-// (-DIPP_DIAG) may override it through the environment; the product build
-// reads no environment at all.
 #ifdef IPP_DIAG
 inline int diag_env(const char* name, int dflt) {
     const char* e = getenv(name);
     return e ? atoi(e) : dflt;
 }
-inline int copy_blocks_per_item() {
-    static const int v = [] {
-        const int k = diag_env("IPP_COPY_BLOCKS", 4);
-        return k < 1 ? 1 : (k > 64 ? 64 : k);
-    }();
-    return v;
-}
-#else
-constexpr int copy_blocks_per_item() { return 4; }
 #endif
 
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
@@ -672,6 +660,120 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
     }
 }
 
+// Grouped background copy (round 5).  Items are background-sorted, so runs
+// of consecutive items paste onto the same background.  A copy block takes
+// one row slab of a group of kCopyGroup consecutive items: each thread loads a
+// 16-B background vector once and stores it to every item of the run whose
+// composite takes it — outside the item's overlay bands [vb0, vb1), or (column
+// split) outside the overlay's 16-pixel groups [gx0, gx1) in a band row.  The
+// copy's load instructions, which queue on the same texture path as the H
+// pass's gathers, drop by the run length.  Items whose composite is not flat
+// (pitches, alignment) take bg_copy_outside_bands with share = slab.
+#ifndef IPP_COPY_GROUP
+#define IPP_COPY_GROUP IPP_PIPE_COPY_GROUP  // (ipp.h; experiment builds may override it)
+#endif
+#ifndef IPP_COPY_SLABS
+#define IPP_COPY_SLABS (4 * IPP_COPY_GROUP)
+#endif
+#ifndef IPP_COPY_GU
+#define IPP_COPY_GU 4
+#endif
+constexpr int kCopyGroup = IPP_COPY_GROUP;  // items per copy group (≤ 64: one lane per item)
+constexpr int kCopySlabs = IPP_COPY_SLABS;  // copy blocks (row slabs) per group
+static_assert(kCopyGroup >= 1 && kCopyGroup <= 64, "one lane per item of a copy group");
+
+// Item j of a copy group: its composite's flat-copy parameters (lane j).
+struct CopyItem {
+    uint32_t dlo, dhi;        // dst + dst_off
+    uint32_t blo, bhi;        // bg + bg_off
+    int32_t dims;             // bg_w | bg_h << 16 (the run key with the bg pointer)
+    int32_t vb0, vb1;         // overlay bands
+    int32_t c0, c1;           // band-row vectors [c0, c1) left to the V pass
+    int32_t flat;             // composite is a flat 16-B aligned copy of bg
+};
+
+template <int NT = 256, int U = IPP_COPY_GU>
+__device__ __forceinline__ void bg_copy_group(const ipp_pipe_desc* __restrict__ descs, int n, int i0, int slab,
+                                              const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst) {
+    const int cnt = min(kCopyGroup, n - i0);
+    if (cnt <= 0) return;
+    const int lane = threadIdx.x & 63;
+    CopyItem ci = {0u, 0u, 0u, 0u, -1, 0, 0, 0, 0, 0};
+    if (lane < cnt) {
+        const ipp_paste_desc& p = descs[i0 + lane].p;
+        const int rb = 3 * p.bg_w;
+        const uint8_t* sb = bg + p.bg_off;
+        uint8_t* db = dst + p.dst_off;
+        const uint64_t du = reinterpret_cast<uint64_t>(db), bu = reinterpret_cast<uint64_t>(sb);
+        ci.dlo = (uint32_t)du;
+        ci.dhi = (uint32_t)(du >> 32);
+        ci.blo = (uint32_t)bu;
+        ci.bhi = (uint32_t)(bu >> 32);
+        ci.dims = p.bg_w | (p.bg_h << 16);
+        int vb0, vb1, gx0, gx1;
+        paste_bands(p, vb0, vb1);
+        ci.vb0 = vb0;
+        ci.vb1 = vb1;
+        const bool split = band_cols_split(p, bg, dst, gx0, gx1);
+        ci.c0 = split ? 3 * gx0 : 0;
+        ci.c1 = split ? 3 * gx1 : rb / 16;
+        ci.flat = p.bg_pitch == rb && p.dst_pitch == rb && (rb & 15) == 0 && ((du | bu) & 15u) == 0 &&
+                  p.bg_w < 65536 && p.bg_h < 32768 &&
+                  (int64_t)((p.bg_h + kCopySlabs - 1) / kCopySlabs) * (rb / 16) < (1 << 24);  // umulhi exact
+    }
+    auto rl = [](int32_t v, int j) { return __builtin_amdgcn_readlane(v, j); };
+    auto rlu = [](uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int32_t)v, j); };
+    int j0 = 0;
+    while (j0 < cnt) {
+        // run [j0, j1): consecutive items on one background (same pointer and dims)
+        const uint32_t blo = rlu(ci.blo, j0), bhi = rlu(ci.bhi, j0);
+        const int32_t dims = rl(ci.dims, j0);
+        int j1 = j0 + 1;
+        while (j1 < cnt && rlu(ci.blo, j1) == blo && rlu(ci.bhi, j1) == bhi && rl(ci.dims, j1) == dims) ++j1;
+        // flat items of the run: one shared load per vector
+        uint64_t fm = 0;
+        for (int j = j0; j < j1; ++j) fm |= (uint64_t)(rl(ci.flat, j) != 0) << j;
+        if (fm) {
+            const int bw = dims & 0xFFFF, bh = dims >> 16;
+            const int rv = 3 * bw / 16;  // vectors per row
+            const int ya = (int)((int64_t)bh * slab / kCopySlabs), ye = (int)((int64_t)bh * (slab + 1) / kCopySlabs);
+            const uint32_t total = (uint32_t)((ye - ya) * rv);
+            const uint32_t mag = (uint32_t)((0x100000000ull + rv - 1) / rv);  // i / rv = umulhi(i, mag), i < 2^24
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4* s4 = reinterpret_cast<const u32x4*>(((uint64_t)bhi << 32) | blo) + (int64_t)ya * rv;
+            for (uint32_t ib = threadIdx.x; ib < total; ib += U * NT) {
+                u32x4 v[U];
+                int32_t row[U], col[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t i = ib + NT * u;
+                    const uint32_t q = __umulhi(i, mag);
+                    row[u] = ya + (int32_t)q;
+                    col[u] = (int32_t)(i - q * (uint32_t)rv);
+                    if (i < total) v[u] = s4[i];
+                }
+                for (int j = j0; j < j1; ++j) {
+                    if (!((fm >> j) & 1u)) continue;
+                    const int32_t vb0 = rl(ci.vb0, j), vb1 = rl(ci.vb1, j), c0 = rl(ci.c0, j), c1 = rl(ci.c1, j);
+                    u32x4* d4 = reinterpret_cast<u32x4*>(((uint64_t)rlu(ci.dhi, j) << 32) | rlu(ci.dlo, j)) +
+                                (int64_t)ya * rv;
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t i = ib + NT * u;
+                        const bool inside = (uint32_t)(row[u] - vb0) < (uint32_t)(vb1 - vb0) &&
+                                            (uint32_t)(col[u] - c0) < (uint32_t)(c1 - c0);
+                        if (i < total && !inside) __builtin_nontemporal_store(v[u], d4 + i);
+                    }
+                }
+            }
+        }
+        // the run's other items: their own copy, this block's slab of it
+        for (int j = j0; j < j1; ++j)
+            if (!((fm >> j) & 1u)) bg_copy_outside_bands<NT>(descs[i0 + j].p, bg, dst, slab, kCopySlabs);
+        j0 = j1;
+    }
+}
+
 // One H-pass block: band tb of item im.
 template <int NR, bool ZONES, int CN>
 __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __restrict__ src,
@@ -776,26 +878,29 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
 template <int NR, bool ZONES, int CN>
 __global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES ? 3 : 4)))
 k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
-              const ipp_pipe_desc* __restrict__ descs, int tiles_y, ipp_hsv_params hp, const uint8_t* __restrict__ bg,
-              uint8_t* __restrict__ dst, int cpi) {
+              const ipp_pipe_desc* __restrict__ descs, int n, int tiles_y, ipp_hsv_params hp,
+              const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst) {
     __shared__ Hpass2Lds<NR> L;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    // tiles_y = H-pass blocks per item.  Each item owns tiles_y H-pass
-    // blocks followed by cpi background-copy blocks, so the copies run beside
-    // the H pass on every XCD.
-    const int per_item = tiles_y + cpi;
-    const int im = b / per_item;
-    const int tb = b - im * per_item;
-    if (tb >= tiles_y) {
+    // tiles_y = H-pass blocks per item.  Each group of kCopyGroup items owns
+    // its items' H-pass blocks followed by kCopySlabs background-copy blocks,
+    // so the copies run beside the H pass on every XCD.
+    const int per_grp = kCopyGroup * tiles_y + kCopySlabs;
+    const int grp = b / per_grp;
+    const int t = b - grp * per_grp;
+    if (t >= kCopyGroup * tiles_y) {
 #if !(defined(IPP_DIAG) && defined(IPP_DIAG_NOCOPY))  // diagnostic (wrong output): no background copy
-        bg_copy_outside_bands<64 * HP_NW>(descs[im].p, bg, dst, tb - tiles_y, cpi);
+        bg_copy_group<64 * HP_NW>(descs, n, grp * kCopyGroup, t - kCopyGroup * tiles_y, bg, dst);
 #endif
         return;
     }
 #if defined(IPP_DIAG) && defined(IPP_DIAG_COPY_ONLY)
     return;  // diagnostic (wrong output): the copy blocks alone
 #endif
-    hpass_block<NR, ZONES, CN>(L, src, tmp, coefs, descs, im, tb, hp);
+    const int j = t / tiles_y;
+    const int im = grp * kCopyGroup + j;
+    if (im >= n) return;
+    hpass_block<NR, ZONES, CN>(L, src, tmp, coefs, descs, im, t - j * tiles_y, hp);
 }
 
 // V pass on MFMA (tap tiles aligned with 16-row background bands: the plan's
@@ -1130,10 +1235,10 @@ void launch_hpass(int n, int ty, hipStream_t s, const uint8_t* src, uint8_t* tmp
 #else
     constexpr size_t pad = 0;
 #endif
-    // H pass + the background rows outside the overlay bands
-    const int cpi = copy_blocks_per_item();
-    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), dim3((uint32_t)(n * (ty + cpi))), dim3(64 * HP_NW), pad,
-                       s, src, tmp, coefs, descs, ty, hp, bg, dst, cpi);
+    // H pass + the background outside the overlays, per group of kCopyGroup items
+    const int64_t groups = (n + kCopyGroup - 1) / kCopyGroup;
+    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), dim3((uint32_t)(groups * (kCopyGroup * ty + kCopySlabs))),
+                       dim3(64 * HP_NW), pad, s, src, tmp, coefs, descs, n, ty, hp, bg, dst);
 }
 
 template <int NR>
@@ -1161,7 +1266,8 @@ extern "C" int ipp_pipe_hpass_bgcopy(const uint8_t* src, uint8_t* tmp, const int
     if (src_cn != 3 && src_cn != 4) return IPP_E_ARG;
     if (tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;
     const int ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
-    if ((int64_t)(ty + copy_blocks_per_item()) * n_images >= INT32_MAX) return IPP_E_ARG;
+    if ((int64_t)(kCopyGroup * ty + kCopySlabs) * ((n_images + kCopyGroup - 1) / kCopyGroup) >= INT32_MAX)
+        return IPP_E_ARG;
     hipStream_t s = (hipStream_t)stream;
     // Zones are needed unless every range's zone is the whole image (all
     // margins 0).  The source channel count is uniform over the batch.

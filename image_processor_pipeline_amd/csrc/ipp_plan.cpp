@@ -651,6 +651,15 @@ extern "C" int ipp_plan_pipe_batch(const ipp_pipe_plan_cfg* cfg, ipp_pipe_item* 
     std::stable_sort(ord.begin(), ord.end(),
                      [&](int32_t a, int32_t b) { return items[a].bg_index < items[b].bg_index; });
     for (int32_t i = 0; i < n; ++i) descs[i] = d[ord[i]];
+    // The H launch's copy blocks (ipp_pipe.hip bg_copy_group) load each
+    // background vector once per run of same-background items within a group
+    // of IPP_PIPE_COPY_GROUP consecutive items and store it to every item of
+    // the run that takes it: bytes = the composite bytes written + one
+    // background read per (group, run) (IPP_PT_COPY_READS).  (Dense, 16-B aligned images assumed,
+    // as the planner lays them out; other layouts copy per item.)
+    int64_t copy_runs = 0;
+    for (int32_t i = 0; i < n; ++i)
+        copy_runs += (i % IPP_PIPE_COPY_GROUP == 0 || items[ord[i]].bg_index != items[ord[i - 1]].bg_index) ? 1 : 0;
     const int64_t copy_bytes = 2 * 3 * (int64_t)bw * copy_rows + copy_band_bytes;
     totals[IPP_PT_COEF_WORDS] = coef_words;
     totals[IPP_PT_TMP_BYTES] = std::max<int64_t>(tmp_off, 256);
@@ -661,6 +670,7 @@ extern "C" int ipp_plan_pipe_batch(const ipp_pipe_plan_cfg* cfg, ipp_pipe_item* 
     totals[IPP_PT_ALGO_H] = algo_h;
     totals[IPP_PT_ALGO_V] = algo_v;
     totals[IPP_PT_COPY_BYTES] = copy_bytes;
+    totals[IPP_PT_COPY_READS] = copy_runs * 3 * (int64_t)bw * bh;
     totals[IPP_PT_MAX_TILES] = max_tiles;
     return IPP_OK;
 }

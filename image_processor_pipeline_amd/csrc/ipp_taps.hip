@@ -260,8 +260,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             wave_sync();                        // the next window / tile rewrites the area
         }
         if (niter > TAP_NI) {
-            // taps past the register set (scale > 10.5, never a compact tile):
-            // recomputed and stored as bytes over the zeros just written
+            // taps past the register set (scale > 10.5): recomputed and stored
+            // as bytes over the zeros just written, at stage_byte's position for
+            // the tile's layout — compact too (a partial last tile whose few
+            // long-filter outputs keep ≤ 64 nonzero groups over nK ≥ 2 steps)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             uint8_t* tile = reinterpret_cast<uint8_t*>(blk + boff);
             for (int i = TAP_NI; i < niter; ++i) {
@@ -316,8 +318,9 @@ extern "C" int64_t ipp_pipe_taps_scratch_bytes(int32_t n_axes) {
     return align256((int64_t)n_axes * (int64_t)sizeof(ipp_tap_axis)) + 256 + 8 * (int64_t)TAP_FLAG_CAP + TAP_PACK_BYTES;
 }
 
-extern "C" int ipp_pipe_plan_taps(const ipp_tap_axis* axes, int32_t n_axes, int32_t* coefs, void* scratch,
-                                  int64_t* stats, void* stream) {
+extern "C" int ipp_pipe_plan_taps_cap(const ipp_tap_axis* axes, int32_t n_axes, int32_t* coefs, void* scratch,
+                                      int64_t* stats, int64_t pack_cap, void* stream) {
+    if (pack_cap < 0 || pack_cap > TAP_PACK_BYTES) return IPP_E_ARG;
     if (!axes || n_axes <= 0 || !coefs || !scratch || !stats) return IPP_E_ARG;
     for (int32_t j = 0; j < n_axes; ++j) {
         const ipp_tap_axis& a = axes[j];
@@ -373,7 +376,7 @@ extern "C" int ipp_pipe_plan_taps(const ipp_tap_axis* axes, int32_t n_axes, int3
         pbytes += 32 + 64 + (int64_t)hdrs[4 * i + 1] * 3072;
     }
     std::vector<uint8_t> pack;
-    if (pbytes <= TAP_PACK_BYTES) {
+    if (pbytes <= pack_cap) {
         pack.assign((size_t)pbytes, 0);
         int64_t* ph = reinterpret_cast<int64_t*>(pack.data());
         ph[0] = (int64_t)fl.size();
@@ -411,4 +414,9 @@ extern "C" int ipp_pipe_plan_taps(const ipp_tap_axis* axes, int32_t n_axes, int3
     }
     if (hipStreamSynchronize(s) != hipSuccess) return IPP_E_LAUNCH;
     return rc;
+}
+
+extern "C" int ipp_pipe_plan_taps(const ipp_tap_axis* axes, int32_t n_axes, int32_t* coefs, void* scratch,
+                                  int64_t* stats, void* stream) {
+    return ipp_pipe_plan_taps_cap(axes, n_axes, coefs, scratch, stats, TAP_PACK_BYTES, stream);
 }

@@ -213,13 +213,25 @@ typedef struct ipp_pipe_desc {
  * reference chain pipeline.py:526-541 → rotations.py:96, symmetry.py:114-119,
  * filtres_liste.py:84-134, overlays.py:129,138-139).  A composite's rows
  * outside the 16-row bands the overlay touches, [16⌊y/16⌋, 16⌈(y + ov_h)/16⌉),
- * are plain copies of the background (Paste.c leaves them untouched):
+ * are plain copies of the background (Paste.c leaves them untouched), and so
+ * are, inside those bands, the 16-pixel groups outside the overlay's
+ * [⌊x/16⌋, ⌈(x + ov_w)/16⌉) when the composite is dense and 16-B aligned with
+ * a width that is a multiple of 16 (the "column split", one predicate in both
+ * kernels):
  *   ipp_pipe_hpass_bgcopy: the LANCZOS H pass over the virtual cut-out (crop →
  *     rotate → flip → HSV α computed per pixel from the source, never stored)
- *     into the scratch `tmp`, plus the copy of those background rows into
- *     `dst`, spread over copy blocks that run beside the H-pass blocks;
+ *     into the scratch `tmp`, plus the copy of those background bytes into
+ *     `dst` by copy blocks that run beside the H-pass blocks: one block per
+ *     row slab and group of IPP_PIPE_COPY_GROUP consecutive items, each
+ *     background vector loaded once and stored to every item of the group on
+ *     that background;
  *   ipp_pipe_vblend_bands: the V pass over the overlay bands, fused with the
- *     unpremultiply, the alpha blend and the rest of each band's background.
+ *     unpremultiply and the alpha blend; it writes the rest of each band: the
+ *     overlay's 16-pixel groups under the column split, the whole band rows
+ *     otherwise.
+ * The two launches together write every composite byte exactly once: run
+ * both, in this order, on the same dst (either alone leaves part of it
+ * unwritten).
  * src_cn: channels of every source in the batch (3 or 4); hsv: HOST pointer;
  * tap_format: IPP_TAPS_MFMA (V axes planned with transposed = 2 + (p.y mod
  * 16), i.e. tap tiles aligned with 16-row background bands); max_ov_w /
@@ -393,14 +405,24 @@ typedef struct ipp_tap_axis {
 #define IPP_PT_MAX_OV_H 5
 #define IPP_PT_ALGO_H 6       /* algorithmic bytes, see fused.PipePlan        */
 #define IPP_PT_ALGO_V 7
-#define IPP_PT_COPY_BYTES 8
+#define IPP_PT_COPY_BYTES 8   /* 2 x the composite bytes the H launch copies
+                                 (read + write as the V pass would move them;
+                                 dense 16-B aligned images assumed)            */
 #define IPP_PT_MAX_TILES 9
 #define IPP_PT_ERR_ITEM 10    /* on IPP_E_RANGE: global item index and reason: */
 #define IPP_PT_ERR_CODE 11    /* 1 canvas beyond 16.16, 2 ScaleAffine table,
                                  3 degenerate overlay, 4 given parameters do not
                                  fit, 5 H window beyond the LDS ring, 6 empty
                                  randint range                                 */
+#define IPP_PT_COPY_READS 12  /* background bytes the H launch's grouped copy
+                                 loads: one background per run of
+                                 same-background items in each group of
+                                 IPP_PIPE_COPY_GROUP items                     */
 #define IPP_PLAN_TOTALS 16
+
+/* Items per background-copy group of ipp_pipe_hpass_bgcopy (one shared load
+ * per background vector and run of same-background items in the group). */
+#define IPP_PIPE_COPY_GROUP 8
 
 /* items[stop - start]: outputs (inputs too when cfg->given); descs[n] (in
  * processing order), axes[2n]; totals[IPP_PLAN_TOTALS]. */
@@ -420,6 +442,13 @@ int ipp_plan_pipe_batch(const ipp_pipe_plan_cfg* cfg, ipp_pipe_item* items, ipp_
 int64_t ipp_pipe_taps_scratch_bytes(int32_t n_axes);
 int ipp_pipe_plan_taps(const ipp_tap_axis* axes, int32_t n_axes, int32_t* coefs, void* scratch,
                        int64_t* stats, void* stream);
+/* ipp_pipe_plan_taps with the size cap of the one packed upload of the
+ * host-rebuilt tiles given (0 <= pack_cap <= the scratch's pack region, 4 MiB;
+ * ipp_pipe_plan_taps passes the region size).  Rebuilt tiles whose pack
+ * exceeds the cap are copied tile by tile instead; the taps are the same byte
+ * for byte (tests/test_gpu_taps.py forces that path with pack_cap = 0). */
+int ipp_pipe_plan_taps_cap(const ipp_tap_axis* axes, int32_t n_axes, int32_t* coefs, void* scratch,
+                           int64_t* stats, int64_t pack_cap, void* stream);
 /* Host restatement of one tile of that format (Resample.c taps, libm sin):
  * hdr[4], bias[16], blocks (nK·3072 bytes, ≤ blocks_cap).
  * Compact layout (axis->compact, nK >= 2 and at most 64 nonzero 16-column

@@ -111,8 +111,14 @@ def measure(sample: int = 192, size: int = 1024, workload: str = "pipe5") -> dic
     per = max(1, math.ceil(sample / workers))
     tasks = [(1000 + w, per, size, workload) for w in range(workers)]
     ctx = mp.get_context("spawn")
-    with ctx.Pool(workers) as pool:
+    # close + join, not the context manager: Pool.__exit__ terminates the
+    # workers (SIGTERM), which a profiler wrapping the bench logs as aborts
+    pool = ctx.Pool(workers)
+    try:
         res = pool.map(_worker, tasks)
+    finally:
+        pool.close()
+        pool.join()
     wall = max(t for t, _ in res)
     items = sum(c for _, c in res)
     px = 3840 * 2160 if workload == "video4k" else size * size

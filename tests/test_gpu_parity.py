@@ -263,6 +263,34 @@ def test_pipe_odd_background_widths_vs_oracle(D):
             assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (bw, i)
 
 
+def test_pipe_copy_groups_straddling_backgrounds(D):
+    """The H launch's grouped background copy (ipp_pipe.hip bg_copy_group,
+    IPP_PIPE_COPY_GROUP = 8 items per group): 21 items on 4 backgrounds in
+    background-sorted runs of 5-6 items, so groups straddle background
+    changes and the last group holds 5 items; 16-px-multiple background widths
+    (the column split of the band rows) and one that is not; outputs
+    pre-filled with junk, every composite byte equal to the oracle's."""
+    from image_processor_pipeline_amd import fused
+    cfg = fused.PipeConfig(margins=(3, 5, 2, 7), scale_min=0.2, scale_max=0.6)
+    for (bh, bw) in [(70, 256), (66, 200), (40, 125)]:
+        n, K, H, W = 21, 4, 90, 110
+        rng = np.random.default_rng(bh + bw)
+        src = rng.integers(0, 256, (n, H, W, 3), np.uint8)
+        bgs = rng.integers(0, 256, (K, bh, bw, 3), np.uint8)
+        plan = fused.plan_pipe((H, W), n, (bh, bw), K, cfg, seed=bw)
+        runs = np.bincount(plan.items["bg_index"], minlength=K)
+        assert sorted(runs) == [5, 5, 5, 6], runs
+        assert any(e % 8 for e in np.cumsum(runs)[:-1])  # a group of 8 straddles a background change
+        runner = fused.PipeRunner(plan, DEV)
+        a = torch.full((n, bh, bw, 3), 7, dtype=torch.uint8, device=DEV)
+        runner.hpass_bgcopy(_t(src), _t(bgs), a)
+        runner.vblend_bands(_t(bgs), a)
+        torch.cuda.synchronize()
+        got = a.cpu().numpy()
+        for i in range(n):
+            assert np.array_equal(got[i], opipe.pipe_item(src[i], bgs, plan.params[i], cfg)), (bw, i)
+
+
 def test_pipe_wide_overlays_vs_oracle(D):
     """Overlays wider than 560 px (the V pass's overlay rows take most of its
     64 KB of LDS) on an 800-px background."""

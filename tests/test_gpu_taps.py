@@ -74,3 +74,71 @@ def test_device_taps_bench_plan():
     print(f"host-rebuilt tiles: {fixed}")
     assert not bad, bad[:10]
     assert fixed < 2000
+
+
+class _Axes:
+    """A tap plan of hand-made axes (the fields plan_taps reads)."""
+
+    def __init__(self, pairs, compact=1):
+        lib = N.load()
+        self.axes = np.zeros(len(pairs), N.TAP_AXIS)
+        off = 0
+        for j, (n_in, n_out) in enumerate(pairs):
+            ks = lib.ipp_plan_lanczos_ksize(0.0, float(n_in), n_out)
+            a = self.axes[j]
+            a["in_size"], a["out_size"], a["compact"] = n_in, n_out, compact
+            a["nkb"] = lib.ipp_plan_mfma_nk_bound(n_in, n_out, ks)
+            a["n_tiles"] = (n_out + 15) // 16
+            a["coef_off"] = off
+            off += (lib.ipp_plan_mfma_size(n_in, n_out, ks) + 3) // 4 * 4
+        self.coef_words = off
+
+
+def test_device_taps_long_filter_compact_last_tile():
+    """Ratios of 10.6-12 (more taps per output than the planner's 64
+    register-held ones) with 1-8 outputs in the last tile: that tile keeps
+    <= 64 nonzero 16-column groups over >= 2 K steps, so it is compact and
+    its taps past the register set go through stage_byte's compact layout
+    (ipp_taps.hip).  Every tile equals the host restatement."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    lib = N.load()
+    pairs = [(n_out * r // 10, n_out) for n_out in (97, 99, 101, 104, 113, 120) for r in (106, 115, 120)]
+    plan = _Axes(pairs)
+    coefs, _ = F.plan_taps(plan, DEV)
+    torch.cuda.synchronize()
+    assert not _check_axes(plan, coefs, range(len(plan.axes)))
+    c = coefs.cpu().numpy()
+    hits = 0
+    for j, (n_in, n_out) in enumerate(pairs):
+        a = plan.axes[j]
+        T, off = int(a["n_tiles"]), int(a["coef_off"])
+        hdr = c[off:off + 4 * T].reshape(T, 4)
+        ks = lib.ipp_plan_lanczos_ksize(0.0, float(n_in), n_out)
+        hits += int(ks > 64 and n_out % 16 and hdr[T - 1][3] == 1 and hdr[T - 1][1] >= 2)
+    assert hits > 0
+
+
+def test_device_taps_per_tile_copies_equal_packed_upload():
+    """The host-rebuilt tiles' fallback upload (one copy pair per tile, taken
+    when their pack exceeds the scratch's pack region; forced here with
+    pack_cap = 0 through ipp_pipe_plan_taps_cap) writes the same taps byte for
+    byte as the packed upload + k_put_tiles of ipp_pipe_plan_taps."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    lib = N.load()
+    plan = F.plan_pipe((1024, 1024), 2048, (1024, 1024), 16, F.PipeConfig(), seed=3)
+    packed, fixed = F.plan_taps(plan, DEV)
+    assert fixed > 0
+    coefs = torch.zeros_like(packed)
+    scratch = torch.empty(int(lib.ipp_pipe_taps_scratch_bytes(len(plan.axes))), dtype=torch.uint8, device=DEV)
+    stats = np.zeros(2, np.int64)
+    st = torch.cuda.current_stream(DEV).cuda_stream
+    N.check(lib.ipp_pipe_plan_taps_cap(N.np_ptr(plan.axes), len(plan.axes), coefs.data_ptr(), scratch.data_ptr(),
+                                       N.np_ptr(stats), 0, st), "ipp_pipe_plan_taps_cap")
+    torch.cuda.synchronize()
+    assert int(stats[0]) == fixed and int(stats[1]) == 0
+    w = plan.coef_words
+    assert torch.equal(coefs[:w], packed[:w])
+    assert lib.ipp_pipe_plan_taps_cap(N.np_ptr(plan.axes), len(plan.axes), coefs.data_ptr(), scratch.data_ptr(),
+                                      N.np_ptr(stats), -1, st) == N.IPP_E_ARG
