@@ -1214,8 +1214,18 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
     }
 }
 
+// V pass occupancy target (waves per SIMD; 0 = the compiler's choice, which
+// is 2 at 168 VGPRs + 52 AGPRs).
+#ifndef IPP_VB_WPE
+#define IPP_VB_WPE 0
+#endif
+#if IPP_VB_WPE > 0
+#define IPP_VB_ATTR __attribute__((amdgpu_waves_per_eu(IPP_VB_WPE)))
+#else
+#define IPP_VB_ATTR
+#endif
 template <int STORE, int DBG = 0>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) IPP_VB_ATTR
 k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
                    const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int tiles_y,
                    int ov_w_max) {

@@ -78,7 +78,11 @@ def plan_rotate_flip(src_dims: Sequence[Tuple[int, int, int]], angles: Sequence[
             bb = G.rotated_bbox(iw, ih, plan)
             if bb is not None and bb[2] > bb[0] and bb[3] > bb[1]:
                 ox, oy, ow, oh = bb[0], bb[1], bb[2] - bb[0], bb[3] - bb[1]
-        pitch = (4 * ow + 15) // 16 * 16
+        # 128-B row pitch (the packed buffer is 256-B aligned): a tile row's
+        # 256-B nontemporal store then covers whole 128-B lines, and only each
+        # row's last line is written partially (16-B pitches split a line
+        # between two tiles at every tile boundary: 12 % more HBM writes)
+        pitch = (4 * ow + 127) // 128 * 128
         d[i]["src_off"] = src_offsets[i] if src_offsets is not None else 0
         d[i]["src_pitch"] = src_pitches[i] if src_pitches is not None else w * cn
         d[i]["src_cn"] = cn

@@ -7,4 +7,5 @@ export TMPDIR=/tmp
 bash tools/profile.sh $TAG --workload $WL --steps 3 --warmup 1 --no-cpu-baseline --no-copy-ceiling "$@" || exit 25
 python tools/prof_summary.py gpurun_out/$TAG > gpurun_out/$TAG/summary.txt
 python tools/pmc_traffic.py gpurun_out/$TAG $WL $NB gpurun_out/pmc_traffic.json
-find gpurun_out/$TAG -name '*counter_collection.csv' -size +4M -delete
+# raw per-dispatch counters and agent listings: summarised above, not kept
+find gpurun_out/$TAG \( -name "*_agent_info.csv" -o -name "*counter_collection.csv" \) -delete
