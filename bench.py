@@ -58,6 +58,8 @@ def parse(argv=None):
     ap.add_argument("--frames", type=int, default=256,
                     help="video4k: 3840x2160 frames per GPU (weak) or in total (strong)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--rot-row-align", type=int, default=128,
+                    help="rotflip: output row pitch alignment in bytes (A/B of the store alignment)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=192)
     ap.add_argument("--no-copy-ceiling", action="store_true")
@@ -352,7 +354,8 @@ def main(argv=None):
         all_syms = [rng.sample(["o", "h", "v", "hv"], 1)[0] for _ in range(n_global)]
         angles, syms = all_angles[start:stop], all_syms[start:stop]
         flips = [D.SYM_FLIP[s_] for s_ in syms]
-        gplan = D.plan_rotate_flip([(S, S, 3)] * B, angles, flips, src_offsets=[i * S * S * 3 for i in range(B)])
+        gplan = D.plan_rotate_flip([(S, S, 3)] * B, angles, flips, src_offsets=[i * S * S * 3 for i in range(B)],
+                                   row_align=args.rot_row_align)
         if args.dry_run:
             digests = {start + i: _digest(src[i].numpy(), np.array([angles[i], flips[i]])) for i in range(B)}
         else:

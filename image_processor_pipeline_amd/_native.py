@@ -16,6 +16,7 @@ from pathlib import Path
 import numpy as np
 
 LIB_PATH = Path(os.environ.get("IPP_LIB_PATH", str(Path(__file__).resolve().parent / "libipp.so")))
+_EXPERIMENT = "IPP_LIB_PATH" in os.environ  # an A/B library named explicitly (tools/ab.sh)
 
 IPP_OK = 0
 IPP_E_ARG = -1
@@ -173,6 +174,8 @@ def load() -> ctypes.CDLL:
     except OSError as e:  # pragma: no cover - environment dependent
         raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
     for name, (res, args) in SIGNATURES.items():
+        if _EXPERIMENT and not hasattr(lib, name):
+            continue  # an experiment build of an older tree (A/B runs) may predate an entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

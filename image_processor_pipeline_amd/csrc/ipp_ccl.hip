@@ -39,12 +39,13 @@
 //                    two lower-right corners (only where both edge flags are
 //                    set), skipping pairs a neighbouring border pixel already
 //                    unites (global atomicMin union-find on P, at roots).
-//   K3-K5 k_ccl_entries, one launch:
-//                    per open entry: R = find(P, G); A[R] += area; P[G] = R;
-//                    then the image's last block: the best open root (area <<
-//                    32 | ~root), the kept component = the better of the open
-//                    and closed bests; bbox from the closed key, or from its
-//                    entries.
+//   K3 k_ccl_resolve per open entry: R = find(P, G); A[R] += area; P[G] = R.
+//   K4 k_ccl_best    per open root: atomicMax of (area << 32 | ~root).
+//   K5 k_ccl_bbox    the kept component = the better of the open and closed
+//                    bests; bbox from the closed key, or from its entries.
+//                    (One launch for K3-K5, the image's last block doing K4
+//                    and K5 over all its entries, ran 0.2 ms slower per
+//                    video4k step: 16 blocks per image are needed there.)
 //   K6 k_ccl_apply / k_ccl_inwords, one wave per tile meeting the output:
 //                    a one-component tile takes its mask words or nothing; a
 //                    tile with several relabels its words (the same
@@ -271,8 +272,8 @@ __device__ __forceinline__ int run_cid(const Par* par, int j) {
 // Scratch layout per image (offsets in the ipp_ccl_work descriptor).
 struct ImgRec {               // per-image record (img_off), zeroed by k_ccl_prep
     u64 ckey;                 // best closed component (closed_key)
-    int32_t root;             // the kept component's root G, or -1 (k_ccl_entries)
-    uint32_t done;            // k_ccl_entries blocks past their resolve share
+    int32_t root;             // the kept component's root G, or -1 (k_ccl_bbox)
+    int32_t pad;
 };
 
 struct TileRec {              // per tile
@@ -743,79 +744,69 @@ k_ccl_border(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __res
     flush_unions(k.P, L, n, lane);
 }
 
-// K3-K5 in one launch (open components only): ENT_BLOCKS blocks per image
-// stride over the image's entries (their count is known only on the device)
-// and resolve them; the image's last block to finish its share (a per-image
-// counter, release/acquire at agent scope) then picks the kept component and
-// its bbox over all the image's entries.
+// Entry kernels (open components only) run ENT_BLOCKS blocks per image
+// striding over the image's entry count (known only on the device).
 constexpr int ENT_BLOCKS = 16;
 
-__device__ __forceinline__ u64 block_max_u64(u64 key, u64* red) {
-    for (int off = 32; off > 0; off >>= 1) {
-        const u64 o = __shfl_xor(key, off);
-        key = o > key ? o : key;
-    }
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = key;
-    __syncthreads();
-    u64 r = red[0];
-#pragma unroll
-    for (int w = 1; w < 4; ++w) r = red[w] > r ? red[w] : r;
-    return r;
-}
-
 __global__ void __launch_bounds__(256)
-k_ccl_entries(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
-              uint8_t* __restrict__ scratch, const int32_t* __restrict__ counts, unsigned long long* __restrict__ best,
-              int32_t* __restrict__ bbox) {
-    __shared__ u64 red[4];
-    __shared__ int4 bred[4];
-    __shared__ uint32_t last;
+k_ccl_resolve(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch,
+              const int32_t* __restrict__ counts) {
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
     const int im = b / ENT_BLOCKS;
-    const int blk = b - im * ENT_BLOCKS;
     const int n = counts[im];
     const Work k = work_of(scratch, works[im]);
-    // K3: R = find(P, G); A[R] += area; P[G] = R
-    for (int e = blk * 256 + threadIdx.x; e < n; e += ENT_BLOCKS * 256) {
+    for (int e = (int)(b - (uint32_t)im * ENT_BLOCKS) * 256 + threadIdx.x; e < n; e += ENT_BLOCKS * 256) {
         const int32_t L = k.entL[e];
         const int32_t R = gfind(k.P, L);
         atomicAdd(k.A + R, k.entA[e]);
         if (R != L) __hip_atomic_store(k.P + L, R, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        last = __hip_atomic_fetch_add(&k.rec->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-               (uint32_t)(ENT_BLOCKS - 1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    __syncthreads();
-    if (!last) return;  // block-uniform
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    // K4: the best open root, area << 32 | ~root
-    u64 key = 0ull;
-    for (int e = threadIdx.x; e < n; e += 256) {
+}
+
+__global__ void __launch_bounds__(256)
+k_ccl_best(const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, const int32_t* __restrict__ counts,
+           unsigned long long* __restrict__ best) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / ENT_BLOCKS;
+    const int n = counts[im];
+    const Work k = work_of(scratch, works[im]);
+    unsigned long long key = 0ull;
+    for (int e = (int)(b - (uint32_t)im * ENT_BLOCKS) * 256 + threadIdx.x; e < n; e += ENT_BLOCKS * 256) {
         const int32_t L = k.entL[e];
-        if (ld(k.P + L) == L) {
-            const u64 kk = ((u64)__hip_atomic_load(k.A + L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32) |
-                           (u64)(0xFFFFFFFFu - (uint32_t)L);
+        if (k.P[L] == L) {
+            const unsigned long long kk =
+                ((unsigned long long)k.A[L] << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)L);
             key = kk > key ? kk : key;
         }
     }
-    const u64 ko = block_max_u64(key, red);
-    if (threadIdx.x == 0) best[im] = ko;
-    // K5: the kept component = the larger of the best open one and the best
-    // closed one (rec.ckey), the smaller root on equal areas; its bbox = the
-    // closed key's tile bbox, or the union of its open entries' tile bboxes
-    const u64 kc = k.rec->ckey;
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(key, off);
+        key = o > key ? o : key;
+    }
+    if ((threadIdx.x & 63) == 0 && key) atomicMax(best + im, key);
+}
+
+// K5: the kept component = the larger of the best open one (best[im]: area
+// << 32 | ~root) and the best closed one (rec.ckey), the smaller root on equal
+// areas; its bbox = the closed key's tile bbox, or the union of its open
+// entries' tile bboxes.  The image's first block records the root for K6.
+__global__ void __launch_bounds__(256)
+k_ccl_bbox(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __restrict__ works,
+           uint8_t* __restrict__ scratch, const int32_t* __restrict__ counts,
+           const unsigned long long* __restrict__ best, int32_t* __restrict__ bbox) {
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / ENT_BLOCKS;
+    const int blk = b - im * ENT_BLOCKS;
+    const Work k = work_of(scratch, works[im]);
+    const u64 ko = best[im], kc = k.rec->ckey;
     const uint32_t ao = (uint32_t)(ko >> 32), ac = (uint32_t)(kc >> 51);
     const int32_t go = ko ? (int32_t)(0xFFFFFFFFu - (uint32_t)ko) : -1;
     const int32_t gc = kc ? (int32_t)(~(uint32_t)(kc >> 24) & 0x7FFFFFu) : -1;
     const bool closed_wins = kc && (!ko || ac > ao || (ac == ao && gc < go));
     const int32_t broot = closed_wins ? gc : go;
-    if (closed_wins) {
-        if (threadIdx.x == 0) {
-            k.rec->root = broot;
+    if (blk == 0 && threadIdx.x == 0) {
+        k.rec->root = broot;
+        if (closed_wins) {
             const Frame f = frame_of(descs[im]);
             const int yb = (gc >> 1) / f.wb;
             const int tx = ((gc >> 1) - yb * f.wb) / (TW / 2), ty = (2 * yb + (gc & 1)) / TH;
@@ -825,15 +816,14 @@ k_ccl_entries(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __re
             bbox[4 * im + 2] = tx * TW + (int)((q >> 12) & 63u) + 1;
             bbox[4 * im + 3] = ty * TH + (int)((q >> 18) & 63u) + 1;
         }
-        return;
     }
+    if (closed_wins || broot < 0) return;
     int4 bb = make_int4(INT32_MAX, INT32_MAX, -1, -1);
-    if (broot >= 0) {
-        for (int e = threadIdx.x; e < n; e += 256) {
-            if (ld(k.P + k.entL[e]) == broot) {
-                const int4 q = k.entB[e];
-                bb = make_int4(min(bb.x, q.x), min(bb.y, q.y), max(bb.z, q.z), max(bb.w, q.w));
-            }
+    const int n = counts[im];
+    for (int e = blk * 256 + threadIdx.x; e < n; e += ENT_BLOCKS * 256) {
+        if (k.P[k.entL[e]] == broot) {
+            const int4 q = k.entB[e];
+            bb = make_int4(min(bb.x, q.x), min(bb.y, q.y), max(bb.z, q.z), max(bb.w, q.w));
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -842,21 +832,11 @@ k_ccl_entries(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __re
         bb.z = max(bb.z, __shfl_xor(bb.z, off));
         bb.w = max(bb.w, __shfl_xor(bb.w, off));
     }
-    if ((threadIdx.x & 63) == 0) bred[threadIdx.x >> 6] = bb;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        k.rec->root = broot;
-#pragma unroll
-        for (int w = 1; w < 4; ++w) {
-            const int4 q = bred[w];
-            bb = make_int4(min(bb.x, q.x), min(bb.y, q.y), max(bb.z, q.z), max(bb.w, q.w));
-        }
-        if (bb.z >= 0) {  // (bbox preset to INT_MAX, INT_MAX, -1, -1 by k_ccl_prep)
-            bbox[4 * im + 0] = bb.x;
-            bbox[4 * im + 1] = bb.y;
-            bbox[4 * im + 2] = bb.z;
-            bbox[4 * im + 3] = bb.w;
-        }
+    if ((threadIdx.x & 63) == 0 && bb.z >= 0) {
+        atomicMin(&bbox[4 * im + 0], bb.x);
+        atomicMin(&bbox[4 * im + 1], bb.y);
+        atomicMax(&bbox[4 * im + 2], bb.z);
+        atomicMax(&bbox[4 * im + 3], bb.w);
     }
 }
 
@@ -1072,7 +1052,6 @@ __global__ void k_ccl_prep(const ipp_ccl_work* __restrict__ works, uint8_t* __re
         ImgRec* rec = reinterpret_cast<ImgRec*>(scratch + works[i].img_off);
         rec->ckey = 0ull;
         rec->root = -1;
-        rec->done = 0u;
     }
 }
 
@@ -1131,7 +1110,9 @@ int run_labels(int src, const uint8_t* img, const ipp_image_desc* descs, int32_t
     }
     hipLaunchKernelGGL(k_ccl_border, L.chunk_grid, dim3(64 * WAVES), 0, s, descs, works, scratch, L.chunks_per_img,
                        n);
-    hipLaunchKernelGGL(k_ccl_entries, L.ent_grid, dim3(256), 0, s, descs, works, scratch, counts, best, bbox);
+    hipLaunchKernelGGL(k_ccl_resolve, L.ent_grid, dim3(256), 0, s, works, scratch, counts);
+    hipLaunchKernelGGL(k_ccl_best, L.ent_grid, dim3(256), 0, s, works, scratch, counts, best);
+    hipLaunchKernelGGL(k_ccl_bbox, L.ent_grid, dim3(256), 0, s, descs, works, scratch, counts, best, bbox);
     return IPP_OK;
 }
 

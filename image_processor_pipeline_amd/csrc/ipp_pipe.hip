@@ -672,9 +672,15 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
 #ifndef IPP_COPY_GROUP
 #define IPP_COPY_GROUP IPP_PIPE_COPY_GROUP  // (ipp.h; experiment builds may override it)
 #endif
+// Copy blocks per group: one per item (A/B, B = 4096, alternating runs on
+// one box: H launch 8.78-8.87 ms at 8 slabs per 8 items, 8.76-8.83 at 6, 8.80-8.88
+// at 4, 8.94 at 16, 9.08-9.10 at 32; per-item copy blocks of round 4: 9.07-9.20;
+// groups of 4 / 12 / 16 items: 8.89-8.90 / 8.84-8.92 / 9.10).
 #ifndef IPP_COPY_SLABS
-#define IPP_COPY_SLABS (4 * IPP_COPY_GROUP)
+#define IPP_COPY_SLABS IPP_COPY_GROUP
 #endif
+// 16-B vectors per thread in flight in the grouped copy (8 spills in the H
+// pass's register budget; 2 measured 0.5 % slower than 4)
 #ifndef IPP_COPY_GU
 #define IPP_COPY_GU 4
 #endif
@@ -743,25 +749,26 @@ __device__ __forceinline__ void bg_copy_group(const ipp_pipe_desc* __restrict__ 
             const u32x4* s4 = reinterpret_cast<const u32x4*>(((uint64_t)bhi << 32) | blo) + (int64_t)ya * rv;
             for (uint32_t ib = threadIdx.x; ib < total; ib += U * NT) {
                 u32x4 v[U];
-                int32_t row[U], col[U];
+                uint32_t rc[U];  // slab row << 16 | vector column (one register per vector)
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t i = ib + NT * u;
                     const uint32_t q = __umulhi(i, mag);
-                    row[u] = ya + (int32_t)q;
-                    col[u] = (int32_t)(i - q * (uint32_t)rv);
+                    rc[u] = (q << 16) | (i - q * (uint32_t)rv);
                     if (i < total) v[u] = s4[i];
                 }
                 for (int j = j0; j < j1; ++j) {
                     if (!((fm >> j) & 1u)) continue;
-                    const int32_t vb0 = rl(ci.vb0, j), vb1 = rl(ci.vb1, j), c0 = rl(ci.c0, j), c1 = rl(ci.c1, j);
+                    // the item's band rows relative to the slab, its band-row vectors [c0, c1)
+                    const int32_t r0 = rl(ci.vb0, j) - ya, rn = rl(ci.vb1, j) - rl(ci.vb0, j);
+                    const int32_t c0 = rl(ci.c0, j), cn = rl(ci.c1, j) - c0;
                     u32x4* d4 = reinterpret_cast<u32x4*>(((uint64_t)rlu(ci.dhi, j) << 32) | rlu(ci.dlo, j)) +
                                 (int64_t)ya * rv;
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const uint32_t i = ib + NT * u;
-                        const bool inside = (uint32_t)(row[u] - vb0) < (uint32_t)(vb1 - vb0) &&
-                                            (uint32_t)(col[u] - c0) < (uint32_t)(c1 - c0);
+                        const bool inside = (uint32_t)((int32_t)(rc[u] >> 16) - r0) < (uint32_t)rn &&
+                                            (uint32_t)((int32_t)(rc[u] & 0xFFFFu) - c0) < (uint32_t)cn;
                         if (i < total && !inside) __builtin_nontemporal_store(v[u], d4 + i);
                     }
                 }
@@ -1214,10 +1221,13 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
     }
 }
 
-// V pass occupancy target (waves per SIMD; 0 = the compiler's choice, which
-// is 2 at 168 VGPRs + 52 AGPRs).
+// V pass occupancy target (waves per SIMD): 3 fits 160 VGPRs without spills
+// (the compiler's own choice, 168 VGPRs + 52 AGPRs, gives 2 waves):
+// ipp_pipe_vblend_bands 1.49-1.52 -> 1.37-1.40 ms (round 5, same box; round
+// 3 measured no difference with the full-width band rows still in the pass).
+// 4 waves spill 54 VGPRs.
 #ifndef IPP_VB_WPE
-#define IPP_VB_WPE 0
+#define IPP_VB_WPE 3
 #endif
 #if IPP_VB_WPE > 0
 #define IPP_VB_ATTR __attribute__((amdgpu_waves_per_eu(IPP_VB_WPE)))

@@ -59,12 +59,13 @@ class GatherPlan:
 def plan_rotate_flip(src_dims: Sequence[Tuple[int, int, int]], angles: Sequence[float],
                      flips: Sequence[int], windows: Optional[Sequence[Tuple[int, int, int, int]]] = None,
                      src_offsets: Optional[Sequence[int]] = None, src_pitches: Optional[Sequence[int]] = None,
-                     crop_to_bbox: bool = True) -> GatherPlan:
+                     crop_to_bbox: bool = True, row_align: int = 128) -> GatherPlan:
     """Plan the fused gather for opaque (3-channel) or alpha-free sources.
 
     src_dims: (h, w, cn) per source; windows: (x0, y0, w, h) crop window per
     source (default: whole image).  The rotated canvas is cropped to its
-    alpha bbox analytically (opaque input ⇒ exact; rotations.py:99-109)."""
+    alpha bbox analytically (opaque input ⇒ exact; rotations.py:99-109).
+    row_align: output row pitch alignment in bytes (a multiple of 16)."""
     n = len(src_dims)
     d = np.zeros(n, N.GATHER_DESC)
     shapes, offs, pitches = [], np.zeros(n, np.int64), np.zeros(n, np.int64)
@@ -82,7 +83,7 @@ def plan_rotate_flip(src_dims: Sequence[Tuple[int, int, int]], angles: Sequence[
         # 256-B nontemporal store then covers whole 128-B lines, and only each
         # row's last line is written partially (16-B pitches split a line
         # between two tiles at every tile boundary: 12 % more HBM writes)
-        pitch = (4 * ow + 127) // 128 * 128
+        pitch = (4 * ow + row_align - 1) // row_align * row_align
         d[i]["src_off"] = src_offsets[i] if src_offsets is not None else 0
         d[i]["src_pitch"] = src_pitches[i] if src_pitches is not None else w * cn
         d[i]["src_cn"] = cn

@@ -128,17 +128,21 @@ def test_device_taps_per_tile_copies_equal_packed_upload():
         pytest.skip("no GPU")
     lib = N.load()
     plan = F.plan_pipe((1024, 1024), 2048, (1024, 1024), 16, F.PipeConfig(), seed=3)
-    packed, fixed = F.plan_taps(plan, DEV)
-    assert fixed > 0
-    coefs = torch.zeros_like(packed)
     scratch = torch.empty(int(lib.ipp_pipe_taps_scratch_bytes(len(plan.axes))), dtype=torch.uint8, device=DEV)
-    stats = np.zeros(2, np.int64)
     st = torch.cuda.current_stream(DEV).cuda_stream
-    N.check(lib.ipp_pipe_plan_taps_cap(N.np_ptr(plan.axes), len(plan.axes), coefs.data_ptr(), scratch.data_ptr(),
-                                       N.np_ptr(stats), 0, st), "ipp_pipe_plan_taps_cap")
-    torch.cuda.synchronize()
-    assert int(stats[0]) == fixed and int(stats[1]) == 0
-    w = plan.coef_words
-    assert torch.equal(coefs[:w], packed[:w])
-    assert lib.ipp_pipe_plan_taps_cap(N.np_ptr(plan.axes), len(plan.axes), coefs.data_ptr(), scratch.data_ptr(),
+    outs, fixed = [], []
+    for cap in (4 << 20, 0):
+        # the same junk in both buffers: bytes the planner leaves alone compare equal
+        coefs = torch.full((plan.coef_words + 4096,), 0x5A5A5A5A, dtype=torch.int32, device=DEV)
+        stats = np.zeros(2, np.int64)
+        N.check(lib.ipp_pipe_plan_taps_cap(N.np_ptr(plan.axes), len(plan.axes), coefs.data_ptr(),
+                                           scratch.data_ptr(), N.np_ptr(stats), cap, st), "ipp_pipe_plan_taps_cap")
+        torch.cuda.synchronize()
+        assert int(stats[1]) == 0
+        outs.append(coefs)
+        fixed.append(int(stats[0]))
+    assert fixed[0] == fixed[1] > 0
+    assert torch.equal(outs[0], outs[1])
+    stats = np.zeros(2, np.int64)
+    assert lib.ipp_pipe_plan_taps_cap(N.np_ptr(plan.axes), len(plan.axes), outs[0].data_ptr(), scratch.data_ptr(),
                                       N.np_ptr(stats), -1, st) == N.IPP_E_ARG
