@@ -267,9 +267,11 @@ def main(argv=None):
     B = stop - start
     FH, FW = 2160, 3840
     scratch_bytes = None
+    reread_bytes = None
     launches = []
     digests = {}
     fused_bound = None
+    bg_copy = None
 
     t_plan = time.perf_counter()
     setup = {}
@@ -311,6 +313,10 @@ def main(argv=None):
             # the H pass also copies the background rows outside the overlay bands
             algo = {"ipp_pipe_hpass_bgcopy": plan.algo_bytes_hpass_bgcopy,
                     "ipp_pipe_vblend_bands": plan.algo_bytes_vblend_bands}
+            # the H launch's copy loads each background vector once per run
+            # of same-background items in a copy group (the formula above
+            # counts one background read per item)
+            bg_copy = {"bg_bytes_loaded": int(plan.copy_read_bytes), "items_per_group": 8}
             launches = [("ipp_pipe_hpass_bgcopy", lambda: runner.hpass_bgcopy(src, bgs, out)),
                         ("ipp_pipe_vblend_bands", lambda: runner.vblend_bands(bgs, out))]
         outputs = lambda: {start + i: _digest(out[i].cpu().numpy()) for i in range(B)}
@@ -332,6 +338,10 @@ def main(argv=None):
             # most, and the per-component scratch are reported apart)
             algo = {"ipp_video_keep_largest": 3 * hw + 4 * a_crop}
             scratch_bytes = B * ((FW + 63) // 64) * ((FH + 63) // 64) * (512 + 1024)
+            # second pass over the crop (k_ccl_inwords + k_ccl_crop_stream):
+            # the BGR crop re-read, its mask words read (8 B per tile row), the
+            # in-words pass's 512 B per tile read and written
+            reread_bytes = 3 * a_crop + a_crop // 8 + a_crop // 4
             launches = [("ipp_video_keep_largest", lambda: chain.run(frames))]
 
             def outputs():
@@ -530,6 +540,10 @@ def main(argv=None):
             result["fused_bound"]["frac_of_copy_ceiling"] = round(gbps / ceiling, 4)
     if scratch_bytes is not None:
         result["label_scratch_bytes_per_step"] = int(scratch_bytes)
+    if reread_bytes is not None:
+        result["crop_reread_bytes_per_step"] = int(reread_bytes)
+    if bg_copy is not None:
+        result["bg_copy"] = bg_copy
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(args)

@@ -78,10 +78,13 @@ class PipePlan:
     max_ov_h: int = 1
     # split form (ipp_pipe_hpass_bgcopy + ipp_pipe_vblend_bands): the
     # composite outside the overlay's 16-pixel groups of its bands moves with
-    # the H pass, written once per item, its background read once per run of
-    # same-background items in a copy group (IPP_PT_COPY_READS)
+    # the H pass.  Algorithmic bytes follow SURVEY §8(d)'s fixed blend formula
+    # (the background read once per item, the composite written once);
+    # copy_read_bytes is what the grouped copy actually loads (one background
+    # per run of same-background items in a copy group, IPP_PT_COPY_READS).
     algo_bytes_hpass_bgcopy: int = 0
     algo_bytes_vblend_bands: int = 0
+    copy_read_bytes: int = 0
 
     @property
     def params(self) -> List[ItemParams]:
@@ -270,7 +273,7 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
     hsv = G.hsv_params(cfg.hsv_ranges, cfg.zones, cfg.use_gimp_scale, bgr=False)
     return PipePlan(descs, axes, T["coef_words"], hsv, items, pool, T["tmp_bytes"], T["max_out_w"], T["max_rows"],
                     bw, bh, T["algo_h"], T["algo_v"], N.IPP_TAPS_MFMA, T["max_ov_w"], T["max_ov_h"],
-                    T["algo_h"] + T["copy_bytes"] // 2 + T["copy_reads"], T["algo_v"] - T["copy_bytes"])
+                    T["algo_h"] + T["copy_bytes"], T["algo_v"] - T["copy_bytes"], T["copy_reads"])
 
 
 def plan_taps(plan: PipePlan, device, stream=None) -> Tuple[torch.Tensor, int]:
