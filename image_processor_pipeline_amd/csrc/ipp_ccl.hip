@@ -156,18 +156,38 @@ typedef uint16_t Par;
 
 __device__ __forceinline__ int lld(const Par* p) { return *reinterpret_cast<const volatile Par*>(p); }
 
+// Physical position of run slot j in the union-find array (experiment
+// switch).  Slot j's dword (two 16-bit entries: rows 2k and 2k+1 of one
+// column pair) sits on bank (column pair) mod 32, so the runs of many rows
+// that start in one column — a blob crossing the tile's left edge, the rows
+// above — hit one bank: that is where k_ccl_label's LDS bank conflicts come
+// from (2.2e8 of 5.9e8 LDS cycles; without the HSV test or the stats atomics
+// they stay, with the mask pass alone they drop to 3e7; profiles/r05/ccl/).
+// Rotating the bank by the row pair (1: add, 2: xor) cuts them to 5.8e7 but
+// costs VALU on every union-find access: 1 made config 5 5 % slower
+// (3.11 -> 3.27 ms), 2 0.3 % slower; the conflicts do not bound the kernel.
+// Both keep each dword's two entries together (lmin16's CAS word).
+#ifndef IPP_CCL_PAR_SWZ
+#define IPP_CCL_PAR_SWZ 0
+#endif
+__device__ __forceinline__ int pswz(int j) {
+    if (IPP_CCL_PAR_SWZ == 2) return j ^ ((j >> 5) & 62);  // bank = column pair ^ row pair
+    if (!IPP_CCL_PAR_SWZ) return j;
+    return (j & ~63) | ((((j >> 1) + (j >> 6)) & 31) << 1) | (j & 1);
+}
+
 __device__ __forceinline__ int lfind(const Par* par, int x) {
-    int p = lld(par + x);
+    int p = lld(par + pswz(x));
     while (p != x) {
         x = p;
-        p = lld(par + x);
+        p = lld(par + pswz(x));
     }
     return x;
 }
 
 // par[b] = min(par[b], a); returns the previous par[b].
 __device__ __forceinline__ int lmin16(Par* par, int b, int a) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(par + (b & ~1));
+    uint32_t* w = reinterpret_cast<uint32_t*>(par + (pswz(b) & ~1));
     const int sh = (b & 1) * 16;
     uint32_t cur = *reinterpret_cast<volatile uint32_t*>(w);
     for (;;) {
@@ -221,7 +241,7 @@ __device__ __forceinline__ int wave_scan_excl(int v, int lane, int& total) {
 // follow (row, run) order — a pure function of the words, so K6 relabelling a
 // tile reproduces K1's ids.
 __device__ __forceinline__ int label_tile(Par* par, int r, int lane, u64 m, u64 p) {
-    for_runs(m, [&](int a, int) { par[slot(r, a)] = slot(r, a); });
+    for_runs(m, [&](int a, int) { par[pswz(slot(r, a))] = slot(r, a); });
     wave_sync();
     if (p) {
         const u64 ps = p & ~(p << 1);
@@ -247,26 +267,26 @@ __device__ __forceinline__ int label_tile(Par* par, int r, int lane, u64 m, u64 
         const int j = slot(r, a);
         const int root = lfind(par, j);
         nroot += root == j;
-        if (root != j) par[j] = root;
+        if (root != j) par[pswz(j)] = root;
     });
     wave_sync();
     int n;
     int cid = wave_scan_excl(nroot, lane, n);
     for_runs(m, [&](int a, int) {
         const int j = slot(r, a);
-        if (par[j] == j) par[j] = NJ + cid++;
+        if (par[pswz(j)] == j) par[pswz(j)] = NJ + cid++;
     });
     wave_sync();
     return n;
 }
 
 __device__ __forceinline__ int run_root(const Par* par, int j) {
-    const int v = par[j];
+    const int v = par[pswz(j)];
     return v >= NJ ? j : v;
 }
 __device__ __forceinline__ int run_cid(const Par* par, int j) {
-    const int v = par[j];
-    return (v >= NJ ? v : par[v]) - NJ;
+    const int v = par[pswz(j)];
+    return (v >= NJ ? v : par[pswz(v)]) - NJ;
 }
 
 // Scratch layout per image (offsets in the ipp_ccl_work descriptor).
@@ -453,12 +473,17 @@ __device__ __forceinline__ void tile_words_quads(const uint8_t* __restrict__ img
             const uint32_t w0 = cur[j].x, w1 = cur[j].y, w2 = cur[j].z;
             const uint32_t px[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 3), __builtin_amdgcn_alignbyte(w2, w1, 2),
                                     w2 >> 8};
+            uint32_t nib = 0;
+#ifdef IPP_CCL_DBG_NOHSV  // diagnostic build (wrong output): fg = blue byte > 100, no table reads
+#pragma unroll
+            for (int k = 0; k < 4; ++k) nib |= ((px[k] & 0xFFu) > 100u ? 1u : 0u) << k;
+#else
             HsvPre pre[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) pre[k] = hsv_pre<NR, true>(*T, px[k]);
-            uint32_t nib = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) nib |= (hsv_post<NR>(*T, pre[k]) == 0u ? 1u : 0u) << k;
+#endif
             // lanes 16rr + q → lane 16rr: 4 → 8 → 16 → 32 bits, then the high half
             uint32_t t = nib | (dpp<0x101>(nib) << 4);      // row_shl:1
             t = t | (dpp<0x102>(t) << 8);                     // row_shl:2
@@ -562,10 +587,11 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
             cols[lane] = 0ull;
         }
         wave_sync();
+#ifndef IPP_CCL_DBG_NOSTATS
         for_runs(m, [&](int a, int len) {
             const int j = slot(r, a);
-            const int v = par[j];
-            const int c = (v >= NJ ? v : par[v]) - NJ - c0;
+            const int v = par[pswz(j)];
+            const int c = (v >= NJ ? v : par[pswz(v)]) - NJ - c0;
             if ((unsigned)c < (unsigned)MAXC) {
                 atomicAdd(&area[c], (uint32_t)len);
                 atomicOr(&rows[c], 1ull << r);
@@ -573,6 +599,9 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
                 if (v >= NJ) croot[c] = j;
             }
         });
+#else  // diagnostic build (wrong output): no per-component stats atomics
+        if (lane < MAXC) croot[lane] = slot(lane, 0);
+#endif
         wave_sync();
         const bool valid = lane < MAXC && c0 + lane < n;
         u64 cm = 0ull, rm = 0ull;
@@ -866,7 +895,7 @@ __device__ __forceinline__ u64 tile_in_word(const Frame& f, const Work& k, int t
     const bool closed_ok = 2ll * f.wb * ((f.h + 1) >> 1) <= CLOSED_SLOTS;
     for_runs(m, [&](int a, int) {
         const int j = slot(lane, a);
-        const int v = par[j];
+        const int v = par[pswz(j)];
         if (v >= NJ) {
             const int c = v - NJ;
             const int32_t G = slot_gidx(f, tx, ty, j);
@@ -1179,6 +1208,9 @@ extern "C" int ipp_video_keep_largest(const uint8_t* frames, const ipp_image_des
     const int rc =
         run_labels(SRC_HSV, frames, descs, n_images, max_w, max_h, hsv, works, scratch, counts, best, bbox, s, L);
     if (rc != IPP_OK) return rc;
+#if defined(IPP_CCL_DBG_NOSTATS) || defined(IPP_CCL_DBG_NOHSV) || defined(IPP_CCL_DBG_MASK_ONLY)
+    return IPP_OK;  // diagnostic builds: labelling only (their bboxes are not valid crops)
+#endif
     hipLaunchKernelGGL(k_ccl_inwords, L.group_grid, dim3(64 * WAVES), 0, s, descs, works, scratch, bbox,
                        L.groups_per_img, L.groups_x);
     hipLaunchKernelGGL(k_ccl_crop_stream, dim3((uint32_t)((int64_t)CROP_BLOCKS * n_images)), dim3(256), 0, s, frames,

@@ -1285,7 +1285,10 @@ extern "C" int ipp_pipe_hpass_bgcopy(const uint8_t* src, uint8_t* tmp, const int
         return IPP_E_ARG;
     if (src_cn != 3 && src_cn != 4) return IPP_E_ARG;
     if (tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;
-    const int ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
+    int ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
+#ifdef IPP_EMPTY_X2
+    ty *= 2;  // experiment: as many empty blocks again (their cost)
+#endif
     if ((int64_t)(kCopyGroup * ty + kCopySlabs) * ((n_images + kCopyGroup - 1) / kCopyGroup) >= INT32_MAX)
         return IPP_E_ARG;
     hipStream_t s = (hipStream_t)stream;
@@ -1342,7 +1345,10 @@ extern "C" int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint
         return IPP_E_ARG;
     const size_t sm = (size_t)VBR * orow_stride(max_ov_w) * sizeof(uint32_t);
     // an overlay of height H at any y spans at most ceil((15 + H) / 16) bands
-    const int tyb = std::min((max_ov_h + 15 + VBR - 1) / VBR, (bg_h + VBR - 1) / VBR);
+    int tyb = std::min((max_ov_h + 15 + VBR - 1) / VBR, (bg_h + VBR - 1) / VBR);
+#ifdef IPP_EMPTY_X2
+    tyb *= 2;  // experiment: as many empty blocks again (their cost)
+#endif
     const int64_t nb = (int64_t)tyb * n_images;
     if (nb >= INT32_MAX || sm > 64 * 1024) return IPP_E_ARG;
     hipStream_t st = (hipStream_t)stream;

@@ -1,4 +1,4 @@
 set -o pipefail
-mkdir -p gpurun_out/r05d
+mkdir -p gpurun_out/r05h
 export TMPDIR=/tmp
-timeout -k 10 1000 bash tools/ab.sh "--steps 20 --warmup 5" r4base g8s8 g8s4 g8s6 g12s8 g8s8vb3 r4base g8s8 g8s4 g8s6 g12s8 g8s8vb3 > gpurun_out/r05d/ab.txt 2>&1; cat gpurun_out/r05d/ab.txt
+timeout -k 10 600 bash tools/ab.sh "--workload video4k --steps 20 --warmup 5" cswz0 cswz2 base cswz0 cswz2 base > gpurun_out/r05h/ab.txt 2>&1; cat gpurun_out/r05h/ab.txt
