@@ -305,20 +305,23 @@ class PipeRunner:
         self.tmp = torch.empty(plan.tmp_bytes, dtype=torch.uint8, device=self.device)
         self.lib = N.load()
 
-    def hpass_bgcopy(self, src: torch.Tensor, bgs: torch.Tensor, out: torch.Tensor) -> None:
-        """H pass + the composite rows outside the overlay bands (split form)."""
+    def hpass_bgcopy(self, src: torch.Tensor, bgs: torch.Tensor, out: torch.Tensor, items=None) -> None:
+        """H pass + the composite rows outside the overlay bands (split form);
+        `items` = (first, count) of the descriptors in processing order."""
         p = self.plan
+        i0, n = items if items is not None else (0, len(p.descs))
         N.check(self.lib.ipp_pipe_hpass_bgcopy(src.data_ptr(), self.tmp.data_ptr(), self.coefs.data_ptr(),
-                                               self.descs.data_ptr(), len(p.descs), p.max_out_w, p.max_rows, 3,
-                                               N.np_ptr(p.hsv), p.tap_format, bgs.data_ptr(), out.data_ptr(),
-                                               _stream(self.device)), "ipp_pipe_hpass_bgcopy")
+                                               self.descs.data_ptr() + i0 * p.descs.itemsize, n, p.max_out_w,
+                                               p.max_rows, 3, N.np_ptr(p.hsv), p.tap_format, bgs.data_ptr(),
+                                               out.data_ptr(), _stream(self.device)), "ipp_pipe_hpass_bgcopy")
 
-    def vblend_bands(self, bgs: torch.Tensor, out: torch.Tensor) -> None:
+    def vblend_bands(self, bgs: torch.Tensor, out: torch.Tensor, items=None) -> None:
         """V pass + paste over the 16-row bands the overlay touches (split form)."""
         p = self.plan
+        i0, n = items if items is not None else (0, len(p.descs))
         N.check(self.lib.ipp_pipe_vblend_bands(self.tmp.data_ptr(), bgs.data_ptr(), out.data_ptr(),
-                                               self.coefs.data_ptr(), self.descs.data_ptr(), len(p.descs), p.bg_w,
-                                               p.bg_h, p.max_ov_w, p.max_ov_h, p.tap_format,
+                                               self.coefs.data_ptr(), self.descs.data_ptr() + i0 * p.descs.itemsize,
+                                               n, p.bg_w, p.bg_h, p.max_ov_w, p.max_ov_h, p.tap_format,
                                                _stream(self.device)), "ipp_pipe_vblend_bands")
 
     def status(self) -> int:
