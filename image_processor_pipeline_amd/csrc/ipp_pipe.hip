@@ -794,6 +794,16 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
     hsv_tables_init<NR>(L.T, hp);
+#if defined(IPP_DIAG) && defined(IPP_DIAG_SETUP2)
+    // diagnostic: the block set-up twice (its cost)
+    __syncthreads();
+    {
+        ipp_hsv_params hq = hp;
+        asm volatile("" : "+v"(hq.r[0].lo[0]));
+        hsv_tables_init<NR>(L.T, hq);
+        __syncthreads();
+    }
+#endif
 
     // Zones: per-lane row bits now, column bits per pixel.  With > 8 ranges
     // the column bounds live in LDS (in registers they spilled).
@@ -917,13 +927,22 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
 // step), B = 64 T rows × 16 overlay columns of one channel (four 16-B T groups
 // per lane give all four channels), D lane l = column l&15, rows 4(l>>4)..+3.
 constexpr int VBR = 16;
+// V pass: column tiles with nK ≤ IPP_VB_DB double-buffer their T groups (the
+// wave's next tile's loads fly during this tile's MFMAs): 1.414-1.418 ->
+// 1.399 ms (round 5, alternating runs on one box); nK = 3 spills 65 VGPRs.
+#ifndef IPP_VB_DB
+#define IPP_VB_DB 2
+#endif
 // V pass: the band's taps loaded once for all its column tiles (nK ≤ 4).
 #ifndef IPP_VB_HOIST
 #define IPP_VB_HOIST 1
 #endif
 // V pass, background loads of the composite phase (experiment switch): 0 =
 // the next step's issued right after this step's stores, 1 = one step ahead
-// and the first step's before the MFMA phase, 2 = one step ahead.
+// and the first step's before the MFMA phase, 2 = one step ahead.  At 3
+// waves/SIMD: 1.400 / 1.416 / 1.422-1.424 ms for 1 / 2 / 0 (round 5, one box;
+// at 2 waves/SIMD 1 was 14 % slower than 2), but 1 spills 2 VGPRs at 3 waves:
+// 2 kept.
 #ifndef IPP_VB_PF
 #define IPP_VB_PF 2
 #endif
@@ -1071,15 +1090,6 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
 #pragma unroll
                 for (int j = 0; j < 4; ++j) g[j] = tq[j * gstride];
             };
-            for (int ct = wave; ct < ctiles; ct += 4) {
-                const int x = 16 * ct + x_l;
-                i32x4 acc[4][3];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    acc[c][0] = i32x4{rb[0], rb[1], rb[2], rb[3]};
-                    acc[c][1] = i32x4{0, 0, 0, 0};
-                    acc[c][2] = i32x4{0, 0, 0, 0};
-                }
 #define IPP_VB_MFMA(a, g)                                                                    \
     {                                                                                        \
         const i32x4 bq[4] = {i32x4{(int)(g)[0].x, (int)(g)[1].x, (int)(g)[2].x, (int)(g)[3].x}, \
@@ -1090,9 +1100,64 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
             _Pragma("unroll") for (int q = 0; q < 3; ++q)                                    \
                 acc[c][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8((a)[q], bq[c], acc[c][q], 0, 0, 0); \
     }
+#define IPP_VB_ACC_INIT                                          \
+    _Pragma("unroll") for (int c = 0; c < 4; ++c) {              \
+        acc[c][0] = i32x4{rb[0], rb[1], rb[2], rb[3]};           \
+        acc[c][1] = i32x4{0, 0, 0, 0};                           \
+        acc[c][2] = i32x4{0, 0, 0, 0};                           \
+    }
+// the tile's unpremultiplied overlay pixels into the band's LDS rows
+#define IPP_VB_EPILOGUE(ct)                                                                     \
+    {                                                                                           \
+        const int x = 16 * (ct) + x_l;                                                          \
+        if (x < p.ov_w) {                                                                       \
+            _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                     \
+                const int row = 4 * (lane >> 4) + r; /* band row = tile row */                  \
+                const int o = y0 + row - p.y;        /* overlay row */                          \
+                if (o >= oy_lo && o < oy_hi) {                                                  \
+                    uint32_t px = 0;                                                            \
+                    _Pragma("unroll") for (int c = 0; c < 4; ++c)                               \
+                        px |= clip8(acc[c][0][r] + (acc[c][1][r] << 8) + (acc[c][2][r] << 16)) << (8 * c); \
+                    orow[row * os + xo + x] = (kVbX & 2) ? px : unpremultiply(px);             \
+                }                                                                               \
+            }                                                                                   \
+        }                                                                                       \
+    }
+            if constexpr (NK > 0 && NK <= IPP_VB_DB) {
+                // double-buffered T groups: the wave's next column tile's
+                // loads are in flight during this tile's MFMAs and epilogue
+                uint4 gc[NK][4], gn[NK][4];
+                int ct = wave;
+                if (ct < ctiles) {
+#pragma unroll
+                    for (int ks = 0; ks < NK; ++ks) tload(ct, ks, gc[ks]);
+                }
+                for (; ct < ctiles; ct += 4) {
+                    const bool more = ct + 4 < ctiles;
+                    if (more) {
+#pragma unroll
+                        for (int ks = 0; ks < NK; ++ks) tload(ct + 4, ks, gn[ks]);
+                    }
+                    i32x4 acc[4][3];
+                    IPP_VB_ACC_INIT
+#pragma unroll
+                    for (int ks = 0; ks < NK; ++ks) IPP_VB_MFMA(ta[ks], gc[ks])
+                    IPP_VB_EPILOGUE(ct)
+                    if (more) {
+#pragma unroll
+                        for (int ks = 0; ks < NK; ++ks)
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) gc[ks][j] = gn[ks][j];
+                    }
+                }
+            } else {
+            for (int ct = wave; ct < ctiles; ct += 4) {
+                i32x4 acc[4][3];
+                IPP_VB_ACC_INIT
                 if (NK > 0) {
                     // (loading the next column tile's T groups here, before
-                    // this tile's MFMAs, measured +9 %)
+                    // this tile's MFMAs, measured +9 % at 2 waves/SIMD; see
+                    // IPP_VB_DB for the double-buffered form)
                     uint4 g[NK > 0 ? NK : 1][4];
 #pragma unroll
                     for (int ks = 0; ks < NK; ++ks) tload(ct, ks, g[ks]);
@@ -1110,22 +1175,12 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
                         IPP_VB_MFMA(a, g)
                     }
                 }
-#undef IPP_VB_MFMA
-                if (x < p.ov_w) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int row = 4 * (lane >> 4) + r;   // band row = tile row
-                        const int o = y0 + row - p.y;           // overlay row
-                        if (o >= oy_lo && o < oy_hi) {
-                            uint32_t px = 0;
-#pragma unroll
-                            for (int c = 0; c < 4; ++c)
-                                px |= clip8(acc[c][0][r] + (acc[c][1][r] << 8) + (acc[c][2][r] << 16)) << (8 * c);
-                            orow[row * os + xo + x] = (kVbX & 2) ? px : unpremultiply(px);
-                        }
-                    }
-                }
+                IPP_VB_EPILOGUE(ct)
             }
+            }
+#undef IPP_VB_ACC_INIT
+#undef IPP_VB_EPILOGUE
+#undef IPP_VB_MFMA
         };
         switch (IPP_VB_HOIST ? th.y : 0) {
             case 1: tiles(std::integral_constant<int, 1>{}); break;
