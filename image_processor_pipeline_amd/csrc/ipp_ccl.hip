@@ -436,6 +436,12 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
 }
 
+// Mask pass: pixel slots whose 64 pixels all have the wave's reference
+// colour skip the HSV test (3.12 -> 2.98 ms per config-5 step, round 5,
+// alternating runs on one box; profiles/r05/ccl/ab_uniform_slots_r05n.txt).
+#ifndef IPP_CCL_UNIFORM
+#define IPP_CCL_UNIFORM 1
+#endif
 // Mask words of one interior tile of a 3-channel HSV source (FULL): lane =
 // (row rr = lane >> 4 of a 4-row group, pixel quad q = lane & 15), one 12-byte
 // load per lane and group = 4 pixels (768 contiguous bytes per row group and
@@ -460,6 +466,7 @@ __device__ __forceinline__ void tile_words_quads(const uint8_t* __restrict__ img
 #pragma unroll
     for (int j = 0; j < GB; ++j) bufA[j] = *reinterpret_cast<const u32x3*>(base + j * gstep);
     uint32_t mlo = 0u, mhi = 0u;
+    uint32_t ref_c = 0xFFFFFFFFu, ref_keep = 0u;  // reference colour (none yet) and its nibble
 #pragma unroll
     for (int gb = 0; gb < G / GB; ++gb) {
         u32x3(&cur)[GB] = (gb & 1) ? bufB : bufA;
@@ -478,11 +485,33 @@ __device__ __forceinline__ void tile_words_quads(const uint8_t* __restrict__ img
 #pragma unroll
             for (int k = 0; k < 4; ++k) nib |= ((px[k] & 0xFFu) > 100u ? 1u : 0u) << k;
 #else
-            HsvPre pre[4];
+            // Pixel slots k whose 64 pixels all have the wave's reference
+            // colour (lane 0's first pixel of the group: a frame's flat
+            // background or blob) take its cached result instead of the HSV
+            // test (IPP_CCL_UNIFORM); the others, or all four, the full test.
+            uint32_t need = 0xFu;
+            if (IPP_CCL_UNIFORM) {
+                const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(px[0] & 0xFFFFFFu));
+                need = 0u;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) pre[k] = hsv_pre<NR, true>(*T, px[k]);
+                for (int k = 0; k < 4; ++k) need |= (__builtin_amdgcn_ballot_w64((px[k] & 0xFFFFFFu) != c0) != 0ull) << k;
+                if (need != 0xFu && c0 != ref_c) {  // wave-uniform: the reference colour's result, once
+                    ref_c = c0;
+                    ref_keep = hsv_post<NR>(*T, hsv_pre<NR, true>(*T, c0)) == 0u ? 0xFu : 0u;
+                }
+            }
+            if (need == 0xFu) {
+                HsvPre pre[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) nib |= (hsv_post<NR>(*T, pre[k]) == 0u ? 1u : 0u) << k;
+                for (int k = 0; k < 4; ++k) pre[k] = hsv_pre<NR, true>(*T, px[k]);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) nib |= (hsv_post<NR>(*T, pre[k]) == 0u ? 1u : 0u) << k;
+            } else {
+                nib = ref_keep & ~need;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if ((need >> k) & 1u) nib |= (hsv_post<NR>(*T, hsv_pre<NR, true>(*T, px[k])) == 0u ? 1u : 0u) << k;
+            }
 #endif
             // lanes 16rr + q → lane 16rr: 4 → 8 → 16 → 32 bits, then the high half
             uint32_t t = nib | (dpp<0x101>(nib) << 4);      // row_shl:1

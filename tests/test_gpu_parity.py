@@ -522,6 +522,45 @@ def test_video_chain_random_colour_frames_vs_oracle(D):
             assert res[i].shape[0] * res[i].shape[1] > 0.5 * h * w
 
 
+def test_video_chain_uniform_colour_slots_vs_oracle(D):
+    """The mask pass's reference-colour shortcut (ipp_ccl.hip
+    IPP_CCL_UNIFORM: a pixel slot whose 64 pixels all have lane 0's colour
+    takes that colour's cached result): flat kept and flat excluded
+    backgrounds, single odd pixels in every slot of a lane's 4 pixels and
+    on the reference pixel itself (column 64k, row 4j), a colour change
+    between row groups (the cache refreshes), and a pixel one bit away from
+    the reference colour next to it (the comparison is over its 24 bits, not
+    the loaded dword's fourth byte, which belongs to the next pixel)."""
+    from image_processor_pipeline_amd import geometry as G
+    from image_processor_pipeline_amd.video_chain import VideoChain
+    rng = np.random.default_rng(12)
+    keep = np.array([220, 140, 40], np.uint8)
+    drop = np.array([24, 18, 30], np.uint8)
+    h, w, n = 192, 256, 4
+    fr = np.empty((n, h, w, 3), np.uint8)
+    fr[0], fr[1] = keep, drop
+    fr[2, :96], fr[2, 96:] = keep, drop                     # colour change between row groups
+    fr[3] = drop
+    fr[3, 40:150, 30:200] = keep                            # a kept blob on a dark background
+    for i in range(n):
+        for x in (0, 1, 2, 3, 64, 127, 128, 255):           # slots 0-3, the reference pixel
+            for y in (0, 4, 5, 63, 64, 100, 191):
+                fr[i, y, x] = rng.integers(0, 256, 3)
+        fr[i, 8, 65] = fr[i, 8, 64] ^ np.array([0, 0, 1], np.uint8)
+    chain = VideoChain(n, h, w, DEV)
+    chain.run(_t(fr))
+    res = chain.results()
+    for i in range(n):
+        try:
+            exp = ops.keep_largest_component(ops.color_mask_bgra(fr[i], G.REFERENCE_HSV_RANGES))
+        except ValueError:  # no foreground: the reference raises, the chain gives no crop
+            exp = None
+        if exp is None:
+            assert res[i] is None, i
+        else:
+            assert res[i] is not None and np.array_equal(res[i], exp), i
+
+
 # --------------------------------------------------------------------------- config 5: 4K video chain
 
 def test_video_chain_4k_vs_oracle(D):
