@@ -684,6 +684,13 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
 #ifndef IPP_COPY_GU
 #define IPP_COPY_GU 4
 #endif
+// Store form of the grouped copy: 0 = global nontemporal store, 1 = plain,
+// else a buffer store with these cache-policy bits.  B = 4096, one box,
+// alternating: 9.02-9.03 (0) / 9.35 (1) / 8.98-9.00 (2: nt) / 8.98-9.00 (3:
+// sc0 nt) / 9.41 (16: sc1) / 9.07 (18: sc1 nt) ms for the H launch.
+#ifndef IPP_COPY_STPOL
+#define IPP_COPY_STPOL 2
+#endif
 constexpr int kCopyGroup = IPP_COPY_GROUP;  // items per copy group (≤ 64: one lane per item)
 constexpr int kCopySlabs = IPP_COPY_SLABS;  // copy blocks (row slabs) per group
 static_assert(kCopyGroup >= 1 && kCopyGroup <= 64, "one lane per item of a copy group");
@@ -769,7 +776,15 @@ __device__ __forceinline__ void bg_copy_group(const ipp_pipe_desc* __restrict__ 
                         const uint32_t i = ib + NT * u;
                         const bool inside = (uint32_t)((int32_t)(rc[u] >> 16) - r0) < (uint32_t)rn &&
                                             (uint32_t)((int32_t)(rc[u] & 0xFFFFu) - c0) < (uint32_t)cn;
-                        if (i < total && !inside) __builtin_nontemporal_store(v[u], d4 + i);
+                        if (i < total && !inside) {
+#if IPP_COPY_STPOL == 0
+                            __builtin_nontemporal_store(v[u], d4 + i);
+#elif IPP_COPY_STPOL == 1
+                            d4[i] = v[u];
+#else
+                            __builtin_amdgcn_raw_buffer_store_b128(v[u], rsrc_of(d4), i * 16u, 0, IPP_COPY_STPOL);
+#endif
+                        }
                     }
                 }
             }
