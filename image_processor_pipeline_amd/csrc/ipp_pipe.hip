@@ -943,12 +943,21 @@ k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const 
 // per lane give all four channels), D lane l = column l&15, rows 4(l>>4)..+3.
 constexpr int VBR = 16;
 // V pass: column tiles with nK ≤ IPP_VB_DB double-buffer their T groups (the
-// wave's next tile's loads fly during this tile's MFMAs): 1.414-1.418 ->
-// 1.399 ms (round 5, alternating runs on one box); nK = 3 spills 65 VGPRs.
+// wave's next tile's loads fly during this tile's MFMAs).  At 3 waves/SIMD
+// with every nK ≤ 4 hoisted, DB 2 took 1.414-1.418 -> 1.399 ms (nK 3 spills
+// 65 VGPRs); at 4 waves (below) only nK 1 is hoisted and double-buffered.
 #ifndef IPP_VB_DB
 #define IPP_VB_DB 2
 #endif
-// V pass: the band's taps loaded once for all its column tiles (nK ≤ 4).
+// V pass: the band's taps loaded once for all its column tiles (nK ≤
+// IPP_VB_HOIST_MAX; larger nK load each K step's taps per column tile).  Of
+// the bench's V tiles 7 % have nK 1, 74 % nK 2, 19 % nK 3.  Hoisting only nK
+// ≤ 2 or only nK 1 lets the pass run at 4 waves/SIMD (128 / 106 VGPRs):
+// 1.402 / 1.547 ms against 1.400 at 3 waves with nK ≤ 4 hoisted (round 5,
+// one box, parity green for all three; profiles/r05/vpass/).
+#ifndef IPP_VB_HOIST_MAX
+#define IPP_VB_HOIST_MAX 4
+#endif
 #ifndef IPP_VB_HOIST
 #define IPP_VB_HOIST 1
 #endif
@@ -1197,11 +1206,18 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
 #undef IPP_VB_EPILOGUE
 #undef IPP_VB_MFMA
         };
-        switch (IPP_VB_HOIST ? th.y : 0) {
+        // (a tile with more K steps than IPP_VB_HOIST_MAX takes the generic loop)
+        switch (IPP_VB_HOIST && th.y <= IPP_VB_HOIST_MAX ? th.y : 0) {
             case 1: tiles(std::integral_constant<int, 1>{}); break;
+#if IPP_VB_HOIST_MAX >= 2
             case 2: tiles(std::integral_constant<int, 2>{}); break;
+#endif
+#if IPP_VB_HOIST_MAX >= 3
             case 3: tiles(std::integral_constant<int, 3>{}); break;
+#endif
+#if IPP_VB_HOIST_MAX >= 4
             case 4: tiles(std::integral_constant<int, 4>{}); break;
+#endif
             default: tiles(std::integral_constant<int, 0>{}); break;
         }
         __syncthreads();
@@ -1291,11 +1307,11 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
     }
 }
 
-// V pass occupancy target (waves per SIMD): 3 fits 160 VGPRs without spills
-// (the compiler's own choice, 168 VGPRs + 52 AGPRs, gives 2 waves):
-// ipp_pipe_vblend_bands 1.49-1.52 -> 1.37-1.40 ms (round 5, same box; round
-// 3 measured no difference with the full-width band rows still in the pass).
-// 4 waves spill 54 VGPRs.
+// V pass occupancy target (waves per SIMD).  With every nK ≤ 4 hoisted, 3
+// fit 160 VGPRs (the compiler's own choice, 168 VGPRs + 52 AGPRs, gave 2
+// waves): 1.49-1.52 -> 1.37-1.40 ms (round 5; round 3 measured no difference
+// with the full-width band rows still in the pass), and 4 spilled 54 VGPRs;
+// with only nK 1 hoisted (IPP_VB_HOIST_MAX) 4 fit 128 VGPRs (5: 50 spills).
 #ifndef IPP_VB_WPE
 #define IPP_VB_WPE 3
 #endif
