@@ -189,6 +189,18 @@ __device__ __forceinline__ void asm_wait(uint32_t (&p)[4], int32_t newer) {
         "s_waitcnt vmcnt(4)\n\t"
         "s_branch 4f\n"
         "2:\n\t"
+#if defined(IPP_DIAG) && defined(IPP_DIAG_X3)
+        "s_cmp_eq_u32 %4, 2\n\t"
+        "s_cbranch_scc0 3f\n\t"
+        "s_waitcnt vmcnt(2)\n\t"
+        "s_branch 4f\n"
+        "3:\n\t"
+        "s_cmp_eq_u32 %4, 1\n\t"
+        "s_cbranch_scc0 5f\n\t"
+        "s_waitcnt vmcnt(1)\n\t"
+        "s_branch 4f\n"
+        "5:\n\t"
+#endif
         "s_cmp_eq_u32 %4, 0\n\t"
         "s_cbranch_scc0 4f\n\t"
         "s_waitcnt vmcnt(0)\n"
@@ -228,6 +240,17 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
     // diagnostic (wrong output): no gathers, pixel values from the offsets
 #pragma unroll
     for (int k = 0; k < 4; ++k) { o.p[k] = off[k] * 0x9E3779B1u; asm volatile("" : "+v"(o.p[k])); }
+#elif defined(IPP_DIAG) && defined(IPP_DIAG_X3)
+    // diagnostic (wrong output): one 12-byte load at the lane's first pixel
+    {
+        typedef uint32_t u32x3v __attribute__((ext_vector_type(3)));
+        u32x3v v;
+        asm volatile("buffer_load_dwordx3 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off[0]), "s"(B.rsv));
+        o.p[0] = v.x;
+        o.p[1] = v.y;
+        o.p[2] = v.z;
+        o.p[3] = v.x;
+    }
 #elif defined(IPP_DIAG) && defined(IPP_DIAG_GATHER_L1)
     // diagnostic (wrong output): the same gathers folded into a 16 KB window
 #pragma unroll
@@ -240,6 +263,11 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
     o.live = true;
 }
 
+#if defined(IPP_DIAG) && defined(IPP_DIAG_X3)
+constexpr int kLoadsPerSet = 1;  // diagnostic (wrong output): one 12-byte load per lane and step
+#else
+constexpr int kLoadsPerSet = 4;
+#endif
 constexpr int HP_NW = 4;              // waves per block (one 16-row band)
 constexpr int HP_STEPC = 16 * HP_NW;  // M columns per block-wide phase-1 step
 
@@ -411,11 +439,11 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // copies, and copying a register whose load is in flight waits for it.
         for (int st = 0; st < nsteps; st += 3) {
             iss(st + 2, RC);
-            process(RA, st, 4 * (RB.live + RC.live));
+            process(RA, st, kLoadsPerSet * (RB.live + RC.live));
             iss(st + 3, RA);
-            process(RB, st + 1, 4 * (RC.live + RA.live));
+            process(RB, st + 1, kLoadsPerSet * (RC.live + RA.live));
             iss(st + 4, RB);
-            process(RC, st + 2, 4 * (RA.live + RB.live));
+            process(RC, st + 2, kLoadsPerSet * (RA.live + RB.live));
         }
 
         // The chunk's first tap loads (issued before its gathers) and the bias
@@ -545,9 +573,15 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // The next chunk's first sets are waited for here, at the end of
         // phase 2 (which hid their latency): from this point on the compiler
         // may copy their registers (it does, at the loop's back edge).
+#if defined(IPP_DIAG) && defined(IPP_DIAG_X3)
+        asm_wait(RA.p, RA.live ? kLoadsPerSet * RB.live : -1);
+        asm_wait(RB.p, RB.live ? 0 : -1);
+        if (!more) break;
+#else
         asm_wait(RA.p, RA.live ? 4 * RB.live : -1);
         asm_wait(RB.p, RB.live ? 0 : -1);
         if (!more) break;
+#endif
         __syncthreads();
     }
 }
