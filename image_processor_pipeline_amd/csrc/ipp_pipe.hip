@@ -701,8 +701,10 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
 // composite takes it — outside the item's overlay bands [vb0, vb1), or (column
 // split) outside the overlay's 16-pixel groups [gx0, gx1) in a band row.  The
 // copy's load instructions, which queue on the same texture path as the H
-// pass's gathers, drop by the run length.  Items whose composite is not flat
-// (pitches, alignment) take bg_copy_outside_bands with share = slab.
+// pass's gathers, drop by the run length (its stores stay: they are most of
+// the ≈ 1.4 ms the copy still adds to the H launch).  Items
+// whose composite is not flat (pitches, alignment) take bg_copy_outside_bands
+// with share = slab.
 #ifndef IPP_COPY_GROUP
 #define IPP_COPY_GROUP IPP_PIPE_COPY_GROUP  // (ipp.h; experiment builds may override it)
 #endif
@@ -713,8 +715,8 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
 #ifndef IPP_COPY_SLABS
 #define IPP_COPY_SLABS IPP_COPY_GROUP
 #endif
-// 16-B vectors per thread in flight in the grouped copy (8 spills in the H
-// pass's register budget; 2 measured 0.5 % slower than 4)
+// 16-B vectors per thread in flight in the grouped copy (8 made the kernel
+// spill inside the H pass's 128-VGPR budget; 2 measured 0.5 % slower than 4)
 #ifndef IPP_COPY_GU
 #define IPP_COPY_GU 4
 #endif
