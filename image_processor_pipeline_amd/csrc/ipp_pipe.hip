@@ -269,6 +269,11 @@ constexpr int kLoadsPerSet = 1;  // diagnostic (wrong output): one 12-byte load 
 constexpr int kLoadsPerSet = 4;
 #endif
 constexpr int HP_NW = 4;              // waves per block (one 16-row band)
+#if defined(IPP_DIAG) && defined(IPP_DIAG_NOSYNC)
+#define IPP_HP_SYNC() ((void)0)  // diagnostic (wrong output): no chunk barriers
+#else
+#define IPP_HP_SYNC() __syncthreads()
+#endif
 constexpr int HP_STEPC = 16 * HP_NW;  // M columns per block-wide phase-1 step
 
 // Sticky status of the pipe kernels (ipp_pipe_status): bit 0 = an H-pass
@@ -474,7 +479,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // registers and broke parity.)
         issue(ck, 0, xxl, yyl, RA);
         issue(ck, 1, xxl + sx, yyl + sy, RB);
-        __syncthreads();
+        IPP_HP_SYNC();
 
         // Phase 2 (mfma): wave w takes tile s0 + w; A = 16 window rows × 64
         // columns of one channel (lane l: row l&15, bytes 16(l>>4)..+15),
@@ -582,7 +587,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         asm_wait(RB.p, RB.live ? 0 : -1);
         if (!more) break;
 #endif
-        __syncthreads();
+        IPP_HP_SYNC();
     }
 }
 
