@@ -316,7 +316,8 @@ def main(argv=None):
             # the H launch's copy loads each background vector once per run
             # of same-background items in a copy group (the formula above
             # counts one background read per item)
-            bg_copy = {"bg_bytes_loaded": int(plan.copy_read_bytes), "items_per_group": 8}
+            from image_processor_pipeline_amd import _native
+            bg_copy = {"bg_bytes_loaded": int(plan.copy_read_bytes), "items_per_group": _native.IPP_PIPE_COPY_GROUP}
             launches = [("ipp_pipe_hpass_bgcopy", lambda: runner.hpass_bgcopy(src, bgs, out)),
                         ("ipp_pipe_vblend_bands", lambda: runner.vblend_bands(bgs, out))]
         outputs = lambda: {start + i: _digest(out[i].cpu().numpy()) for i in range(B)}

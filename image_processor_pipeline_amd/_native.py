@@ -109,6 +109,7 @@ TAP_AXIS = np.dtype([
 
 # ipp_plan_pipe_batch totals[] slots (ipp.h IPP_PT_*)
 IPP_PLAN_TOTALS = 16
+IPP_PIPE_COPY_GROUP = 8   # items per background-copy group of ipp_pipe_hpass_bgcopy (ipp.h)
 PT = dict(coef_words=0, tmp_bytes=1, max_out_w=2, max_rows=3, max_ov_w=4, max_ov_h=5, algo_h=6, algo_v=7,
           copy_bytes=8, max_tiles=9, err_item=10, err_code=11, copy_reads=12)
 

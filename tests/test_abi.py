@@ -93,3 +93,13 @@ def test_product_library_reads_no_environment():
     out = subprocess.run([nm, "-D", "--undefined-only", str(N.LIB_PATH)], capture_output=True, text=True,
                          check=True).stdout
     assert "getenv" not in out and "secure_getenv" not in out
+
+
+def test_header_constants_match_the_python_mirror():
+    """#define constants the host code mirrors (plan totals, copy group)."""
+    src = HEADER.read_text()
+    consts = dict(re.findall(r"#define (IPP_[A-Z0-9_]+) (-?\d+)", src))
+    assert int(consts["IPP_PLAN_TOTALS"]) == N.IPP_PLAN_TOTALS
+    assert int(consts["IPP_PIPE_COPY_GROUP"]) == N.IPP_PIPE_COPY_GROUP
+    for name, slot in N.PT.items():
+        assert int(consts["IPP_PT_" + name.upper()]) == slot, name
