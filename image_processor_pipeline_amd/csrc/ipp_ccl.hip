@@ -240,12 +240,26 @@ __device__ __forceinline__ int wave_scan_excl(int v, int lane, int& total) {
 #ifndef IPP_CCL_JUMP
 #define IPP_CCL_JUMP 1
 #endif
+// Tiles where no run touches the row above skip the unions and the root
+// pass: 2.957 -> 2.934 ms per config-5 step (round 5, alternating runs).
+#ifndef IPP_CCL_FASTNOU
+#define IPP_CCL_FASTNOU 1
+#endif
 // Tile labelling on the mask words (lane r: word m of row r, p of row r-1).
 // On return par[slot] holds, for a root run, NJ + its component id, and for
 // any other run its root's slot; returns the component count.  Component ids
 // follow (row, run) order — a pure function of the words, so K6 relabelling a
 // tile reproduces K1's ids.
 __device__ __forceinline__ int label_tile(Par* par, int r, int lane, u64 m, u64 p) {
+    if (IPP_CCL_FASTNOU && __builtin_amdgcn_ballot_w64((m & (p | (p << 1) | (p >> 1))) != 0ull) == 0ull) {
+        // No run touches a run of the row above (a tile of isolated specks):
+        // every run is a root, and the ids follow (row, run) order as below.
+        int n;
+        int cid = wave_scan_excl(__popcll(m & ~(m << 1)), lane, n);
+        for_runs(m, [&](int a, int) { par[pswz(slot(r, a))] = NJ + cid++; });
+        wave_sync();
+        return n;
+    }
     for_runs(m, [&](int a, int) { par[pswz(slot(r, a))] = slot(r, a); });
     wave_sync();
     if (p) {
