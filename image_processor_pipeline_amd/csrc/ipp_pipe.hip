@@ -1356,6 +1356,11 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
 #ifndef IPP_VB_WPE
 #define IPP_VB_WPE 3
 #endif
+// Composite store policy (store16): plain / sc1 / nt 1.335 / 1.581 / 1.356 ms
+// (round 5, alternating runs on one box, profiles/r05/vpass/ab_vstore_policy_r05af.txt).
+#ifndef IPP_VB_STPOL
+#define IPP_VB_STPOL 0
+#endif
 #if IPP_VB_WPE > 0
 #define IPP_VB_ATTR __attribute__((amdgpu_waves_per_eu(IPP_VB_WPE)))
 #else
@@ -1483,15 +1488,14 @@ extern "C" int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint
     // experiment kernels (WRONG output): 9 no background reads, 10 no V pass, 11 stores only
     static const int pol = diag_env("IPP_VB_STORE", 2);
     switch (pol) {
-        case 9: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 1>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-        case 10: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 2>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-        case 11: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 3>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-        default: hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 0>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        case 9: hipLaunchKernelGGL((k_pipe_vblend_mfma<IPP_VB_STPOL, 1>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        case 10: hipLaunchKernelGGL((k_pipe_vblend_mfma<IPP_VB_STPOL, 2>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        case 11: hipLaunchKernelGGL((k_pipe_vblend_mfma<IPP_VB_STPOL, 3>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
+        default: hipLaunchKernelGGL((k_pipe_vblend_mfma<IPP_VB_STPOL, 0>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
     }
 #else
-    // nt stores: the write-once composite does not evict the shared backgrounds
-    hipLaunchKernelGGL((k_pipe_vblend_mfma<2, 0>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs,
-                       descs, tyb, max_ov_w);
+    hipLaunchKernelGGL((k_pipe_vblend_mfma<IPP_VB_STPOL, 0>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst,
+                       coefs, descs, tyb, max_ov_w);
 #endif
     IPP_CHECK_LAUNCH();
     return IPP_OK;
