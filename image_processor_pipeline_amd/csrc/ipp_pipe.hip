@@ -108,9 +108,9 @@ __device__ __forceinline__ uint4 ld_tap(const uint4* base, int idx) {
 // Block = one 16-row band of one item, 4 waves.  It sweeps the item's output
 // tiles in chunks of ≤ 4 tiles whose input window fits the 512-column
 // channel-planar LDS ring.  Phase 1 gathers the chunk's new M columns into
-// the ring (16 columns × 16 rows per wave and step; a lane quad takes a 2×2
-// block of M pixels, whose source pixels lie within ~1.5 px of each other);
-// phase 2 runs the taps on the matrix cores.
+// the ring (16 columns × 16 rows per wave and step; a lane takes 4
+// consecutive M columns of one row, i.e. the ring dword it writes); phase 2
+// runs the taps on the matrix cores.
 // (An LDS-staged form — coalesced source spans, dense HSV — was bit-exact but
 // 1.6× slower, VALU-bound: DESIGN.md §3, profiles/r03_staged/.)
 // ---------------------------------------------------------------------------
@@ -210,8 +210,20 @@ __device__ __forceinline__ void asm_wait(uint32_t (&p)[4], int32_t newer) {
         : "scc");
 }
 
+// A lane's four pixels of a step: 4 consecutive M columns (IPP_HP_CONSEC, the
+// ring's dword as gathered), or columns 2 apart with the partner lane holding
+// the others (a lane quad = a 2×2 block of M pixels; pair_regroup then swaps
+// them into consecutive columns).
+// Consecutive columns: no pair exchange (2 VALU per pixel), H launch
+// 8.79-8.81 -> 8.74-8.76 ms (round 5, alternating runs on one box,
+// profiles/r05/ab_gather_consec_r05aj.txt).
+#ifndef IPP_HP_CONSEC
+#define IPP_HP_CONSEC 1
+#endif
+constexpr int kPixStep = IPP_HP_CONSEC ? 1 : 2;
+
 // Gathers of one live step: xx/yy = 16.16 source position of the lane's
-// first pixel (its next three are 2 columns apart).  Out-of-window pixels load
+// first pixel (its next three are kPixStep columns apart).  Out-of-window pixels load
 // offset 0xFFFFFFFF (the range check returns 0).
 template <int CN, bool CLAMP>
 __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32_t yy, Raw4& o) {
@@ -233,8 +245,8 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
         off[k] = ok ? (o1 & ~3u) : 0xFFFFFFFFu;  // diagnostic (wrong output): dword-aligned gathers
 #endif
         any |= ok;
-        xx += (uint32_t)(2 * B.b0);
-        yy += (uint32_t)(2 * B.b3);
+        xx += (uint32_t)(kPixStep * B.b0);
+        yy += (uint32_t)(kPixStep * B.b3);
     }
 #if defined(IPP_DIAG) && defined(IPP_DIAG_NOGATHER)
     // diagnostic (wrong output): no gathers, pixel values from the offsets
@@ -335,7 +347,9 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     int filled = hdr[0].x;  // ring holds M columns [.., filled)
     Hp2Chunk ck = hp2_chunk(hdr, 0, ntiles, filled, wave);
     // Lane's first column of step 0 and its source position.
-    auto lane_x = [&](const Hp2Chunk& c) { return c.c0 + 16 * wave + 8 * ((lane >> 2) & 1) + (lane & 1); };
+    auto lane_x = [&](const Hp2Chunk& c) {
+        return c.c0 + 16 * wave + 8 * ((lane >> 2) & 1) + (IPP_HP_CONSEC ? 4 : 1) * (lane & 1);
+    };
     // (24-bit products: columns < 2^15 and |b| ≤ 2^16; a 32-bit product made
     // the compiler use a 64-bit mad whose unused high addend was a register
     // that can still be in flight)
@@ -393,7 +407,8 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // newer = gather loads issued after P's (4 per live later set)
         auto process = [&](Raw4& P, int st, int newer) {
             asm_wait(P.p, P.live ? newer : -1);
-            // after the pair exchange lane dx holds columns 8gc + 4dx .. +3
+            // lane dx holds columns 8gc + 4dx .. +3 (after the pair exchange
+            // when the pixels are 2 columns apart)
             const int cg = wave * 4 + 4 * HP_NW * st + 2 * ((lane >> 2) & 1) + (lane & 1);
             const int x = c0 + 4 * cg;
             const bool active = (cg < ng4) && (r < nrows);
@@ -403,7 +418,8 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                 zb[k] = ~0u;
                 if (ZONES) {
                     // column of gather k's pixel (before the pair exchange)
-                    const int xk = c0 + 16 * wave + HP_STEPC * st + 8 * ((lane >> 2) & 1) + (lane & 1) + 2 * k;
+                    const int xk = c0 + 16 * wave + HP_STEPC * st + 8 * ((lane >> 2) & 1) +
+                                   (IPP_HP_CONSEC ? 4 : 1) * (lane & 1) + kPixStep * k;
                     zb[k] = 0;
 #pragma unroll
                     for (int q = 0; q < NR; ++q) zb[k] |= (uint32_t)((uint32_t)(xk - zc0[q]) < (uint32_t)zcw[q]) << q;
@@ -420,12 +436,12 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                     if (CLAMP) raw >>= ((P.fl >> (1 + k)) & 1u) << 3;
                     px[k] = hsv2_px<NR, ZONES>(T, raw, zb[k]);
                 }
-                pair_regroup(px, lane & 1);
+                if (!IPP_HP_CONSEC) pair_regroup(px, lane & 1);
                 transpose4(px[0], px[1], px[2], px[3], ch);
             } else if (ZONES) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) px[k] = hsv2_px<NR, ZONES>(T, 0u, zb[k]);
-                pair_regroup(px, lane & 1);
+                if (!IPP_HP_CONSEC) pair_regroup(px, lane & 1);
                 transpose4(px[0], px[1], px[2], px[3], ch);
             } else {
 #pragma unroll
@@ -937,7 +953,7 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
 
     __syncthreads();  // tables visible
     // Fill value (raw 0): uniform over the block except for zone bits.
-    const uint32_t fill = hsv2_px<NR, ZONES>(L.T, 0u, ~0u);
+    const uint32_t fill = __builtin_amdgcn_readfirstlane(hsv2_px<NR, ZONES>(L.T, 0u, ~0u));  // (in an SGPR)
     const int nrows = min(HR, h.lines - row0);
     if (CN == 3 && clamp)
         hpass2_body<NR, ZONES, CN, true>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
