@@ -91,6 +91,24 @@ __device__ __forceinline__ uint32_t unpremultiply(uint32_t px) {
     return out;
 }
 
+// unpremultiply with the per-α division by a magic multiplier: M[a] =
+// floor(2^31 / a) + 1 gives floor(255·c / a) = (510·c · M[a]) >> 32 exactly
+// for every a in 1..255 and c in 0..255 (checked exhaustively by
+// tests/test_host_plan.py::test_unpremultiply_magic_table_is_exact).  M[0] is
+// unused (α 0 returns the pixel, as above).
+__host__ __device__ constexpr uint32_t unpremul_magic(uint32_t a) { return a ? (uint32_t)((1ull << 31) / a + 1ull) : 0u; }
+__device__ __forceinline__ uint32_t unpremultiply_magic(uint32_t px, const uint32_t* __restrict__ M) {
+    const uint32_t a = px >> 24;
+    const uint32_t m = M[a];
+    uint32_t out = a << 24;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const uint32_t q = __umulhi(510u * ((px >> (8 * c)) & 0xFFu), m);
+        out |= (q > 255u ? 255u : q) << (8 * c);
+    }
+    return a == 0u ? px : out;
+}
+
 // Resample.c clip8: clamp(ss >> 22, 0, 255) with an arithmetic shift.
 //
 // The empty asm is an optimisation barrier: ROCm 7.2's gfx950 backend fuses

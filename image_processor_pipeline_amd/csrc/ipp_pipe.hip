@@ -1003,6 +1003,13 @@ constexpr int VBR = 16;
 // wave's next tile's loads fly during this tile's MFMAs).  At 3 waves/SIMD
 // with every nK ≤ 4 hoisted, DB 2 took 1.414-1.418 -> 1.399 ms (nK 3 spills
 // 65 VGPRs); at 4 waves (below) only nK 1 is hoisted and double-buffered.
+// Unpremultiply by a per-block LDS table of magic divisors (exact,
+// unpremultiply_magic) instead of a reciprocal and two fix-ups per channel:
+// 1.340 -> 1.319 ms (round 5, alternating runs on one box,
+// profiles/r05/vpass/ab_unpremul_magic_r05al.txt).
+#ifndef IPP_VB_MAGIC
+#define IPP_VB_MAGIC 1
+#endif
 #ifndef IPP_VB_DB
 #define IPP_VB_DB 2
 #endif
@@ -1128,6 +1135,11 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
     uint4 gcur[3];
     if (IPP_VB_PF == 1 && groups && (int)threadIdx.x < gtotal) gload(threadIdx.x, gcur);
     if (any) {
+        uint32_t* umag = orow + VBR * os;  // IPP_VB_MAGIC: the unpremultiply divisors
+        if (IPP_VB_MAGIC) {
+            umag[threadIdx.x] = unpremul_magic(threadIdx.x);
+            __syncthreads();
+        }
         // zero the ≤ 15 columns before the overlay and the 16 after it
         for (int e = threadIdx.x; e < VBR * 32; e += 256) {
             const int row = e >> 5, c = e & 31;
@@ -1199,7 +1211,7 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
                     uint32_t px = 0;                                                            \
                     _Pragma("unroll") for (int c = 0; c < 4; ++c)                               \
                         px |= clip8(acc[c][0][r] + (acc[c][1][r] << 8) + (acc[c][2][r] << 16)) << (8 * c); \
-                    orow[row * os + xo + x] = (kVbX & 2) ? px : unpremultiply(px);             \
+                    orow[row * os + xo + x] = (kVbX & 2) ? px : IPP_VB_MAGIC ? unpremultiply_magic(px, umag) : unpremultiply(px); \
                 }                                                                               \
             }                                                                                   \
         }                                                                                       \
@@ -1491,7 +1503,7 @@ extern "C" int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint
     if (!tmp || !bg || !dst || !coefs || !descs || n_images < 0 || bg_w <= 0 || bg_h <= 0) return IPP_E_ARG;
     if (tap_format != IPP_TAPS_MFMA || max_ov_w <= 0 || max_ov_w > bg_w || max_ov_h <= 0 || max_ov_h > bg_h)
         return IPP_E_ARG;
-    const size_t sm = (size_t)VBR * orow_stride(max_ov_w) * sizeof(uint32_t);
+    const size_t sm = ((size_t)VBR * orow_stride(max_ov_w) + 256) * sizeof(uint32_t);  // + the magic divisors
     // an overlay of height H at any y spans at most ceil((15 + H) / 16) bands
     int tyb = std::min((max_ov_h + 15 + VBR - 1) / VBR, (bg_h + VBR - 1) / VBR);
 #ifdef IPP_EMPTY_X2

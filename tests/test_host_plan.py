@@ -142,3 +142,15 @@ def test_pipe_plan_copy_read_bytes_follow_the_copy_groups():
         runs = sum(1 for i in range(n) if i % 8 == 0 or order[i] != order[i - 1])
         assert plan.copy_read_bytes == runs * 3 * bw * bh, (n, K)
         assert plan.algo_bytes_hpass_bgcopy > plan.algo_bytes_hpass
+
+
+def test_unpremultiply_magic_table_is_exact():
+    """ipp_device.h unpremultiply_magic: floor(255·c / a) = (510·c · M[a]) >> 32
+    with M[a] = floor(2^31 / a) + 1, for every α 1..255 and channel 0..255
+    (the V pass's unpremultiply, Pillow's RGBa → RGBA integer division)."""
+    c = np.arange(256, dtype=np.uint64)
+    for a in range(1, 256):
+        m = (1 << 31) // a + 1
+        assert m < 1 << 32
+        q = ((np.uint64(510) * c) * np.uint64(m)) >> np.uint64(32)
+        assert np.array_equal(q, (255 * c) // a), a
