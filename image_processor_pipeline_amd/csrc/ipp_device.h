@@ -123,6 +123,26 @@ __device__ __forceinline__ uint32_t clip8(int32_t ss) {
     return (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 
+// Four clip8 results packed into one dword (byte k = clip8(sk)): two
+// v_ashr_pk_u8_i32 (each gives two saturated bytes and leaves bits 16-31 of
+// its register as they were — here undefined, and discarded) and one v_perm
+// taking the low halves; 3 VALU instead of about 11.  In the pipe's H and V
+// epilogues: H launch 8.77 -> 8.64 ms (round 5, alternating runs on one box,
+// profiles/r05/ab_packed_clip_r05ao.txt).
+#ifndef IPP_PK_CLIP
+#define IPP_PK_CLIP 1
+#endif
+__device__ __forceinline__ uint32_t clip8x4(int32_t s0, int32_t s1, int32_t s2, int32_t s3) {
+#if IPP_PK_CLIP
+    uint32_t lo, hi;
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 22" : "=v"(lo) : "v"(s0), "v"(s1));
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 22" : "=v"(hi) : "v"(s2), "v"(s3));
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+#else
+    return clip8(s0) | (clip8(s1) << 8) | (clip8(s2) << 16) | (clip8(s3) << 24);
+#endif
+}
+
 // Python slice(start, stop).indices(length) for step 1 (zone masks,
 // filtres_liste.py:102-103: mask[t : H-b, l : W-r] = 255).
 __device__ __forceinline__ void slice_indices(int start, int stop, int length, int& lo, int& hi) {

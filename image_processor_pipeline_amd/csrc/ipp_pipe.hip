@@ -569,14 +569,14 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             }
             const int xo = 16 * t + (lane & 15);
             if (xo < h.out_len) {
-                uint32_t outc[4] = {0u, 0u, 0u, 0u};
+                uint32_t outc[4];
 #pragma unroll
-                for (int c = 0; c < 4; ++c)
+                for (int c = 0; c < 4; ++c) {
+                    int32_t ss[4];
 #pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        const int32_t ss = acc[c][0][rr] + (acc[c][1][rr] << 8) + (acc[c][2][rr] << 16);
-                        outc[c] |= clip8(ss) << (8 * rr);
-                    }
+                    for (int rr = 0; rr < 4; ++rr) ss[rr] = acc[c][0][rr] + (acc[c][1][rr] << 8) + (acc[c][2][rr] << 16);
+                    outc[c] = clip8x4(ss[0], ss[1], ss[2], ss[3]);
+                }
                 // (an opaque lane copy: hoisted out of the chunk loop, this
                 // 64-bit row address was live through phase 1 and spilled)
                 int ln = lane;
@@ -1208,9 +1208,10 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
                 const int row = 4 * (lane >> 4) + r; /* band row = tile row */                  \
                 const int o = y0 + row - p.y;        /* overlay row */                          \
                 if (o >= oy_lo && o < oy_hi) {                                                  \
-                    uint32_t px = 0;                                                            \
+                    int32_t ss[4];                                                              \
                     _Pragma("unroll") for (int c = 0; c < 4; ++c)                               \
-                        px |= clip8(acc[c][0][r] + (acc[c][1][r] << 8) + (acc[c][2][r] << 16)) << (8 * c); \
+                        ss[c] = acc[c][0][r] + (acc[c][1][r] << 8) + (acc[c][2][r] << 16);      \
+                    const uint32_t px = clip8x4(ss[0], ss[1], ss[2], ss[3]);                    \
                     orow[row * os + xo + x] = (kVbX & 2) ? px : IPP_VB_MAGIC ? unpremultiply_magic(px, umag) : unpremultiply(px); \
                 }                                                                               \
             }                                                                                   \
