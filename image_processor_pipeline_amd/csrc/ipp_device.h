@@ -143,6 +143,29 @@ __device__ __forceinline__ uint32_t clip8x4(int32_t s0, int32_t s1, int32_t s2, 
 #endif
 }
 
+// clip8x4(s) ^ 0x80808080 for s already lowered by 128 << 22 (folded into the
+// MFMA bias): clamp(v - 128, -128, 127) as a byte is clamp(v, 0, 255) ^ 0x80,
+// and v_ashr_pk_i8_i32 saturates to exactly that range.
+__device__ __forceinline__ uint32_t clip8x4_x80(int32_t s0, int32_t s1, int32_t s2, int32_t s3) {
+    uint32_t lo, hi;
+    asm("v_ashr_pk_i8_i32 %0, %1, %2, 22" : "=v"(lo) : "v"(s0), "v"(s1));
+    asm("v_ashr_pk_i8_i32 %0, %1, %2, 22" : "=v"(hi) : "v"(s2), "v"(s3));
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
+// a0 + (a1 << 8) + (a2 << 16) (the three tap byte planes' accumulators) in two
+// v_lshl_add_u32 (the compiler's form was two shifts and an add3).
+__device__ __forceinline__ int32_t planes3(int32_t a0, int32_t a1, int32_t a2) {
+#if IPP_PK_CLIP
+    int32_t t, r;
+    asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(t) : "v"(a1), "v"(a0));
+    asm("v_lshl_add_u32 %0, %1, 16, %2" : "=v"(r) : "v"(a2), "v"(t));
+    return r;
+#else
+    return a0 + (a1 << 8) + (a2 << 16);
+#endif
+}
+
 // Python slice(start, stop).indices(length) for step 1 (zone masks,
 // filtres_liste.py:102-103: mask[t : H-b, l : W-r] = 255).
 __device__ __forceinline__ void slice_indices(int start, int stop, int length, int& lo, int& hi) {

@@ -210,6 +210,11 @@ __device__ __forceinline__ void asm_wait(uint32_t (&p)[4], int32_t newer) {
         : "scc");
 }
 
+// H-pass T bytes by signed saturation of bias-lowered sums (clip8x4_x80).
+#ifndef IPP_PK_T
+#define IPP_PK_T 1
+#endif
+
 // A lane's four pixels of a step: 4 consecutive M columns (IPP_HP_CONSEC, the
 // ring's dword as gathered), or columns 2 apart with the partner lane holding
 // the others (a lane quad = a 2×2 block of M pixels; pair_regroup then swaps
@@ -508,9 +513,10 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         if (has_tile) {
 #endif
             i32x4 acc[4][3];
+            const int32_t b0 = IPP_PK_T ? bias - (128 << 22) : bias;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                acc[c][0] = i32x4{bias, bias, bias, bias};
+                acc[c][0] = i32x4{b0, b0, b0, b0};
                 acc[c][1] = i32x4{0, 0, 0, 0};
                 acc[c][2] = i32x4{0, 0, 0, 0};
             }
@@ -569,13 +575,17 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             }
             const int xo = 16 * t + (lane & 15);
             if (xo < h.out_len) {
+                // T bytes = clip8 ^ 0x80 (the MFMA's signed form); with
+                // IPP_PK_T the ^ 0x80 comes from the signed saturation of
+                // sums lowered by 128 << 22 in the bias (acc init above)
                 uint32_t outc[4];
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     int32_t ss[4];
 #pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) ss[rr] = acc[c][0][rr] + (acc[c][1][rr] << 8) + (acc[c][2][rr] << 16);
-                    outc[c] = clip8x4(ss[0], ss[1], ss[2], ss[3]);
+                    for (int rr = 0; rr < 4; ++rr) ss[rr] = planes3(acc[c][0][rr], acc[c][1][rr], acc[c][2][rr]);
+                    outc[c] = IPP_PK_T ? clip8x4_x80(ss[0], ss[1], ss[2], ss[3])
+                                       : clip8x4(ss[0], ss[1], ss[2], ss[3]) ^ 0x80808080u;
                 }
                 // (an opaque lane copy: hoisted out of the chunk loop, this
                 // 64-bit row address was live through phase 1 and spilled)
@@ -583,8 +593,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                 asm volatile("" : "+v"(ln));
                 const int grp = (row0 >> 2) + (ln >> 4);
                 uint4* dst = reinterpret_cast<uint4*>(tmp + h.dst_off + (int64_t)grp * h.dst_pitch) + xo;
-                const uint32_t w[4] = {outc[0] ^ 0x80808080u, outc[1] ^ 0x80808080u, outc[2] ^ 0x80808080u,
-                                       outc[3] ^ 0x80808080u};
+                const uint32_t w[4] = {outc[0], outc[1], outc[2], outc[3]};
                 // Nontemporal: T is read back only after the whole launch
                 // (-0.8 % against plain stores; nontemporal T loads in the V
                 // pass measured +15 %).
@@ -1210,7 +1219,7 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
                 if (o >= oy_lo && o < oy_hi) {                                                  \
                     int32_t ss[4];                                                              \
                     _Pragma("unroll") for (int c = 0; c < 4; ++c)                               \
-                        ss[c] = acc[c][0][r] + (acc[c][1][r] << 8) + (acc[c][2][r] << 16);      \
+                        ss[c] = planes3(acc[c][0][r], acc[c][1][r], acc[c][2][r]);               \
                     const uint32_t px = clip8x4(ss[0], ss[1], ss[2], ss[3]);                    \
                     orow[row * os + xo + x] = (kVbX & 2) ? px : IPP_VB_MAGIC ? unpremultiply_magic(px, umag) : unpremultiply(px); \
                 }                                                                               \
