@@ -222,6 +222,11 @@ __device__ __forceinline__ void asm_wait(uint32_t (&p)[4], int32_t newer) {
 // Consecutive columns: no pair exchange (2 VALU per pixel), H launch
 // 8.79-8.81 -> 8.74-8.76 ms (round 5, alternating runs on one box,
 // profiles/r05/ab_gather_consec_r05aj.txt).
+// Gathers: the row test by the buffer's range check (H 8.79 -> 8.75 ms,
+// round 5, alternating runs on one box, profiles/r05/ab_gather_yrange_r05ar.txt).
+#ifndef IPP_HP_YRANGE
+#define IPP_HP_YRANGE 1
+#endif
 #ifndef IPP_HP_CONSEC
 #define IPP_HP_CONSEC 1
 #endif
@@ -238,7 +243,12 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int xin = (int32_t)xx >> 16, yin = (int32_t)yy >> 16;
-        const bool ok = ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h);
+        // (IPP_HP_YRANGE: rows outside the window fail the buffer's range
+        // check by themselves — its records end one byte past the window's
+        // last pixel — so only the column is tested; not under CLAMP, whose
+        // offsets are clamped back into range)
+        const bool ok = IPP_HP_YRANGE && !CLAMP ? (uint32_t)xin < (uint32_t)B.in_w
+                                      : ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h);
         uint32_t o1 = (uint32_t)__mul24(yin, B.pitch) + (uint32_t)__umul24((uint32_t)xin, (uint32_t)CN);
         if (CLAMP) {
             const uint32_t offc = min(o1, B.lim);
@@ -922,7 +932,11 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
     const bool clamp = need > nrec;  // last pixel's dword would cross the image end (block-uniform)
     const uint64_t sbu = reinterpret_cast<uint64_t>(S.base);
     Hp2Block B;
-    B.rsv = u32x4_t{(uint32_t)sbu, (uint32_t)(sbu >> 32) & 0xFFFFu, (uint32_t)nrec, 0x00020000u};
+    // records: to the image end, or (IPP_HP_YRANGE) only to one byte past the
+    // window's last pixel, so that a row above or below the window is out of
+    // range (row y ≥ in_h starts at y·pitch ≥ need, as pitch ≥ in_w·CN)
+    const int nrecs = IPP_HP_YRANGE ? min(nrec, need) : nrec;
+    B.rsv = u32x4_t{(uint32_t)sbu, (uint32_t)(sbu >> 32) & 0xFFFFu, (uint32_t)nrecs, 0x00020000u};
     B.lim = S.lim;
     B.rowx = (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1;
     B.rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
