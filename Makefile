@@ -1,5 +1,5 @@
 # Builds the gfx950 HIP C-ABI library in-tree (travels to the GPU box with the
-# snapshot) and the oracle's C helpers.  Usage: make -j8
+# snapshot) and the H pass's ISA for the static hazard check.  Usage: make -j8
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 PKG := image_processor_pipeline_amd
@@ -52,7 +52,16 @@ variant:
 	for f in $(HOST_SRCS); do g++ $(HOSTFLAGS) -c $$f -o variants/$(NAME)/obj/$$(basename $$f .cpp).o || exit 1; done
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o variants/$(NAME)/libipp.so variants/$(NAME)/obj/*.o -lpthread
 
+# A variant that differs only in one kernel file (F, default ipp_pipe): that
+# file rebuilt with VFLAGS, linked with the in-tree objects of the others.
+#   make kvariant NAME=kb2 VFLAGS=-DIPP_HP_BANDS=2 [F=ipp_ccl]
+F ?= ipp_pipe
+kvariant: $(OBJS)
+	mkdir -p variants/$(NAME)/obj
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) $$(echo " $(FPEXACT) " | grep -q " $(F).hip " && echo -ffp-contract=off) -c $(CSRC)/$(F).hip -o variants/$(NAME)/obj/$(F).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o variants/$(NAME)/libipp.so variants/$(NAME)/obj/$(F).o $(filter-out $(OBJDIR)/$(F).o,$(OBJS)) -lpthread
+
 clean:
 	rm -rf build $(LIB)
 
-.PHONY: all clean asm variant
+.PHONY: all clean asm variant kvariant

@@ -54,7 +54,8 @@ def parse(argv=None):
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--backgrounds", type=int, default=16)
-    ap.add_argument("--workload", choices=["pipe5", "rotflip", "video4k"], default="pipe5")
+    ap.add_argument("--workload", choices=["pipe5", "rotflip", "video4k"], default=None,
+                    help="pipe5 (default; with the rotflip and video4k legs unless --no-legs), or one workload alone")
     ap.add_argument("--frames", type=int, default=256,
                     help="video4k: 3840x2160 frames per GPU (weak) or in total (strong)")
     ap.add_argument("--seed", type=int, default=0)
@@ -73,6 +74,11 @@ def parse(argv=None):
                     help="--stream: launch the pipe on the default-priority stream (not a high-priority one)")
     ap.add_argument("--stream-lookahead", type=int, default=2,
                     help="--stream: batches planned ahead of the running one (worker threads, side streams)")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="pipe5: skip the config-2 (rotflip) and config-5 (video4k) legs that the default run "
+                         "times after the headline and reports under 'workloads'")
+    ap.add_argument("--frame-noise", type=int, default=0,
+                    help="video4k: +-N LSB of uniform noise per channel on the synthetic frames (0 = flat frames)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: CPU rehearsal of the N-rank path (tests)")
     ap.add_argument("--dump-digests", default=None,
@@ -250,12 +256,56 @@ def main(argv=None):
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch(args.gpus, argv))
+    legs = args.workload is None and not args.no_legs and not args.dry_run and not args.dump_digests
+    if args.workload is None:
+        args.workload = "pipe5"
 
-    import numpy as np
+    import copy
     import torch
     import torch.distributed as dist
 
     rank, world, dev = init_dist(args)
+    result = run_workload(args, rank, world, dev)
+    if legs and result is not None:
+        # BASELINE configs 2 and 5 on the same box in the same run, each at
+        # its own default size (B = 1024 items; 256 frames per GPU)
+        result["workloads"] = {}
+        for wl in ("rotflip", "video4k"):
+            torch.cuda.empty_cache()
+            a = copy.copy(args)
+            a.workload, a.batch = wl, None
+            r = run_workload(a, rank, world, dev)
+            if r is not None:
+                result["workloads"][wl] = leg_summary(r)
+    if rank == 0 and result is not None:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def leg_summary(r: dict) -> dict:
+    """The compact record of a secondary workload (the driver keeps only the
+    tail of the line): its metric is the headline's, on that workload."""
+    rf = r["roofline"]
+    out = {"value": r["value"], "unit": r["unit"], "ms_per_step": r["ms_per_step"],
+           "batch": r["config"]["global_batch"], "image": r["config"]["image"],
+           "roofline": {k: rf[k] for k in ("kernel", "achieved", "frac", "traffic", "traffic_frac") if k in rf}}
+    out["roofline"]["step_frac"] = rf["step"]["frac"]
+    for k in ("label_scratch_bytes_per_step", "crop_reread_bytes_per_step"):
+        if k in r:
+            out[k] = r[k]
+    if "cpu_baseline" in r:
+        cb = r["cpu_baseline"]
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "cores", "kind", "value_1core") if k in cb}
+    return out
+
+
+def run_workload(args, rank, world, dev):
+    """One workload's timed run; returns its JSON record (rank 0), or None
+    for --dry-run (the digests are written here)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
     from image_processor_pipeline_amd import fused, device as D
 
     S, K = args.size, args.backgrounds
@@ -324,7 +374,7 @@ def main(argv=None):
         workload = "5-stage pipe: crop(64px)->rotate(NEAREST,expand,bbox)->flip->HSV mask(4 ref ranges)->LANCZOS+paste"
     elif args.workload == "video4k":
         from image_processor_pipeline_amd import video_chain
-        frames = video_chain.synthetic_frames(B, FH, FW, args.seed + 2, dev, start=start)
+        frames = video_chain.synthetic_frames(B, FH, FW, args.seed + 2, dev, start=start, noise=args.frame_noise)
         if args.dry_run:
             digests = {start + i: _digest(frames[i].numpy()) for i in range(B)}
         else:
@@ -400,9 +450,7 @@ def main(argv=None):
             print(json.dumps({"metric": METRICS[args.workload], "dry_run": True, "n_gpus": world,
                               "scaling": args.scaling, "global_batch": n_global, "items": len(digests),
                               "plan_ms": round(plan_ms, 1)}), flush=True)
-        if world > 1:
-            dist.destroy_process_group()
-        return
+        return None
 
     ceiling = None
     if not args.no_copy_ceiling:
@@ -485,12 +533,18 @@ def main(argv=None):
     value = mpix * args.steps / elapsed
     achieved = algo[dominant] / (per_kernel_ms[dominant] * 1e-3) / 1e9
     step_algo = sum(algo.values())
+    traffic = load_pmc_traffic(args.workload, dominant, B)
     roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": load_pmc_traffic(args.workload, dominant, B),
+                "traffic": traffic,
                 "algo_bytes_per_launch": int(algo[dominant] / n_launch[dominant]),
                 "avg_launch_ms": round(per_kernel_ms[dominant] / n_launch[dominant], 4),
                 "launches_per_step": n_launch[dominant]}
+    if traffic:
+        # the launch's real HBM rate: its PMC bytes (committed profile of this
+        # workload at this batch) over its HIP-event time, against the peak
+        roofline["traffic_gbps"] = round(traffic / n_launch[dominant] / (roofline["avg_launch_ms"] * 1e-3) / 1e9, 1)
+        roofline["traffic_frac"] = round(roofline["traffic_gbps"] / HBM_PEAK_GBPS, 4)
     if ceiling:
         roofline["copy_ceiling"] = round(ceiling, 1)
         roofline["frac_of_copy_ceiling"] = round(achieved / ceiling, 4)
@@ -550,10 +604,9 @@ def main(argv=None):
             result["cpu_baseline"] = cpu_baseline(args)
         except Exception as e:  # reported, never fatal to the GPU number
             result["cpu_baseline"] = {"error": repr(e)}
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if args.workload == "video4k" and args.frame_noise:
+        result["config"]["frame_noise_lsb"] = args.frame_noise
+    return result
 
 
 if __name__ == "__main__":

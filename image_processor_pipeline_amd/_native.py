@@ -16,7 +16,10 @@ from pathlib import Path
 import numpy as np
 
 LIB_PATH = Path(os.environ.get("IPP_LIB_PATH", str(Path(__file__).resolve().parent / "libipp.so")))
-_EXPERIMENT = "IPP_LIB_PATH" in os.environ  # an A/B library named explicitly (tools/ab.sh)
+# A/B runs of an experiment build of an older tree (tools/ab.sh, gpu_ab.sh)
+# may predate an entry point; only they opt in to skipping (and logging) the
+# missing names.  IPP_LIB_PATH alone still requires every ipp.h entry point.
+_EXPERIMENT = os.environ.get("IPP_AB_EXPERIMENT") == "1"
 
 IPP_OK = 0
 IPP_E_ARG = -1
@@ -110,6 +113,7 @@ TAP_AXIS = np.dtype([
 # ipp_plan_pipe_batch totals[] slots (ipp.h IPP_PT_*)
 IPP_PLAN_TOTALS = 16
 IPP_PIPE_COPY_GROUP = 8   # items per background-copy group of ipp_pipe_hpass_bgcopy (ipp.h)
+IPP_PIPE_MAX_OV_W = 992   # widest overlay of ipp_pipe_vblend_bands (ipp.h)
 PT = dict(coef_words=0, tmp_bytes=1, max_out_w=2, max_rows=3, max_ov_w=4, max_ov_h=5, algo_h=6, algo_v=7,
           copy_bytes=8, max_tiles=9, err_item=10, err_code=11, copy_reads=12)
 
@@ -174,12 +178,17 @@ def load() -> ctypes.CDLL:
         lib = ctypes.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | getattr(os, "RTLD_LOCAL", 0))
     except OSError as e:  # pragma: no cover - environment dependent
         raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+    skipped = []
     for name, (res, args) in SIGNATURES.items():
         if _EXPERIMENT and not hasattr(lib, name):
-            continue  # an experiment build of an older tree (A/B runs) may predate an entry point
+            skipped.append(name)
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if skipped:
+        import sys
+        print(f"_native: IPP_AB_EXPERIMENT: {LIB_PATH} lacks {', '.join(skipped)}", file=sys.stderr)
     _lib = lib
     return lib
 

@@ -156,25 +156,15 @@ typedef uint16_t Par;
 
 __device__ __forceinline__ int lld(const Par* p) { return *reinterpret_cast<const volatile Par*>(p); }
 
-// Physical position of run slot j in the union-find array (experiment
-// switch).  Slot j's dword (two 16-bit entries: rows 2k and 2k+1 of one
-// column pair) sits on bank (column pair) mod 32, so the runs of many rows
-// that start in one column — a blob crossing the tile's left edge, the rows
-// above — hit one bank: that is where k_ccl_label's LDS bank conflicts come
-// from (2.2e8 of 5.9e8 LDS cycles; without the HSV test or the stats atomics
-// they stay, with the mask pass alone they drop to 3e7; profiles/r05/ccl/).
-// Rotating the bank by the row pair (1: add, 2: xor) cuts them to 5.8e7 but
-// costs VALU on every union-find access: 1 made config 5 5 % slower
-// (3.11 -> 3.27 ms), 2 0.3 % slower; the conflicts do not bound the kernel.
-// Both keep each dword's two entries together (lmin16's CAS word).
-#ifndef IPP_CCL_PAR_SWZ
-#define IPP_CCL_PAR_SWZ 0
-#endif
-__device__ __forceinline__ int pswz(int j) {
-    if (IPP_CCL_PAR_SWZ == 2) return j ^ ((j >> 5) & 62);  // bank = column pair ^ row pair
-    if (!IPP_CCL_PAR_SWZ) return j;
-    return (j & ~63) | ((((j >> 1) + (j >> 6)) & 31) << 1) | (j & 1);
-}
+// Physical position of run slot j in the union-find array.  Slot j's dword
+// (two 16-bit entries: rows 2k and 2k+1 of one column pair) sits on bank
+// (column pair) mod 32, so the runs of many rows that start in one column — a
+// blob crossing the tile's left edge — hit one bank: that is where
+// k_ccl_label's LDS bank conflicts come from (2.2e8 of 5.9e8 LDS cycles;
+// profiles/r05/ccl/).  Rotating the bank by the row pair cut them to 5.8e7 but
+// cost VALU on every union-find access: config 5 0.3-5 % slower (round 5, two
+// forms measured), so slots stay in place.
+__device__ __forceinline__ int pswz(int j) { return j; }
 
 __device__ __forceinline__ int lfind(const Par* par, int x) {
     int p = lld(par + pswz(x));
@@ -235,23 +225,16 @@ __device__ __forceinline__ int wave_scan_excl(int v, int lane, int& total) {
     return s - v;
 }
 
-// Pointer jumping after the unions (below): 2.998 -> 2.978 ms per config-5
-// step (round 5, alternating runs on one box).
-#ifndef IPP_CCL_JUMP
-#define IPP_CCL_JUMP 1
-#endif
-// Tiles where no run touches the row above skip the unions and the root
-// pass: 2.957 -> 2.934 ms per config-5 step (round 5, alternating runs).
-#ifndef IPP_CCL_FASTNOU
-#define IPP_CCL_FASTNOU 1
-#endif
+// (Pointer jumping after the unions: 2.998 -> 2.978 ms per config-5 step;
+// tiles where no run touches the row above skip the unions and the root
+// pass: 2.957 -> 2.934 ms; round 5, alternating runs on one box.)
 // Tile labelling on the mask words (lane r: word m of row r, p of row r-1).
 // On return par[slot] holds, for a root run, NJ + its component id, and for
 // any other run its root's slot; returns the component count.  Component ids
 // follow (row, run) order — a pure function of the words, so K6 relabelling a
 // tile reproduces K1's ids.
 __device__ __forceinline__ int label_tile(Par* par, int r, int lane, u64 m, u64 p) {
-    if (IPP_CCL_FASTNOU && __builtin_amdgcn_ballot_w64((m & (p | (p << 1) | (p >> 1))) != 0ull) == 0ull) {
+    if (__builtin_amdgcn_ballot_w64((m & (p | (p << 1) | (p >> 1))) != 0ull) == 0ull) {
         // No run touches a run of the row above (a tile of isolated specks):
         // every run is a root, and the ids follow (row, run) order as below.
         int n;
@@ -281,7 +264,6 @@ __device__ __forceinline__ int label_tile(Par* par, int r, int lane, u64 m, u64 
         });
     }
     wave_sync();
-#if IPP_CCL_JUMP
     // Pointer jumping: the unions of a column of runs (a blob crossing the
     // tile: each row's run linked under the row above's) leave chains as long
     // as the tile is tall, and the root pass below would walk them lane by
@@ -301,7 +283,6 @@ __device__ __forceinline__ int label_tile(Par* par, int r, int lane, u64 m, u64 
         wave_sync();
         if (__builtin_amdgcn_ballot_w64(moved) == 0ull) break;
     }
-#endif
     int nroot = 0;
     for_runs(m, [&](int a, int) {
         const int j = slot(r, a);
@@ -477,11 +458,9 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
 }
 
 // Mask pass: pixel slots whose 64 pixels all have the wave's reference
-// colour skip the HSV test (3.12 -> 2.98 ms per config-5 step, round 5,
-// alternating runs on one box; profiles/r05/ccl/ab_uniform_slots_r05n.txt).
-#ifndef IPP_CCL_UNIFORM
-#define IPP_CCL_UNIFORM 1
-#endif
+// colour skip the HSV test (3.12 -> 2.98 ms per config-5 step on flat
+// synthetic frames, round 5, alternating runs on one box;
+// profiles/r05/ccl/ab_uniform_slots_r05n.txt).
 // Mask words of one interior tile of a 3-channel HSV source (FULL): lane =
 // (row rr = lane >> 4 of a 4-row group, pixel quad q = lane & 15), one 12-byte
 // load per lane and group = 4 pixels (768 contiguous bytes per row group and
@@ -521,16 +500,12 @@ __device__ __forceinline__ void tile_words_quads(const uint8_t* __restrict__ img
             const uint32_t px[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 3), __builtin_amdgcn_alignbyte(w2, w1, 2),
                                     w2 >> 8};
             uint32_t nib = 0;
-#ifdef IPP_CCL_DBG_NOHSV  // diagnostic build (wrong output): fg = blue byte > 100, no table reads
-#pragma unroll
-            for (int k = 0; k < 4; ++k) nib |= ((px[k] & 0xFFu) > 100u ? 1u : 0u) << k;
-#else
             // Pixel slots k whose 64 pixels all have the wave's reference
             // colour (lane 0's first pixel of the group: a frame's flat
             // background or blob) take its cached result instead of the HSV
-            // test (IPP_CCL_UNIFORM); the others, or all four, the full test.
+            // test; the others, or all four, the full test.
             uint32_t need = 0xFu;
-            if (IPP_CCL_UNIFORM) {
+            {
                 const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(px[0] & 0xFFFFFFu));
                 need = 0u;
 #pragma unroll
@@ -552,7 +527,6 @@ __device__ __forceinline__ void tile_words_quads(const uint8_t* __restrict__ img
                 for (int k = 0; k < 4; ++k)
                     if ((need >> k) & 1u) nib |= (hsv_post<NR>(*T, hsv_pre<NR, true>(*T, px[k])) == 0u ? 1u : 0u) << k;
             }
-#endif
             // lanes 16rr + q → lane 16rr: 4 → 8 → 16 → 32 bits, then the high half
             uint32_t t = nib | (dpp<0x101>(nib) << 4);      // row_shl:1
             t = t | (dpp<0x102>(t) << 8);                     // row_shl:2
@@ -572,15 +546,11 @@ __device__ __forceinline__ void tile_words_quads(const uint8_t* __restrict__ img
     p = lane > 0 ? p : 0ull;
 }
 
-// K1: one wave per 64×64 tile, WAVES tiles side by side per block.
-#ifndef IPP_CCL_WPE  // K1 occupancy target (waves per SIMD; 0 = the compiler's choice): 6 → 49-55 VGPRs, 7 waves/SIMD, no spills; 3.44 vs 3.63 ms per video4k step (the default choice was 85-89 VGPRs, 5 waves)
-#define IPP_CCL_WPE 6
-#endif
+// K1: one wave per 64×64 tile, WAVES tiles side by side per block.  Occupancy
+// target 6 waves per SIMD: 49-55 VGPRs, 7 waves/SIMD, no spills; 3.44 vs 3.63
+// ms per video4k step against the compiler's choice (85-89 VGPRs, 5 waves).
 template <int SRC, int NR, bool ZONES>
-__global__ void __launch_bounds__(64 * WAVES)
-#if IPP_CCL_WPE
-__attribute__((amdgpu_waves_per_eu(IPP_CCL_WPE)))
-#endif
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(6)))
 k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
             const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch, int32_t* __restrict__ counts,
             int groups_per_img, int groups_x, ipp_hsv_params hp) {
@@ -624,11 +594,6 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
         tile_words<SRC, NR, ZONES, true>(img, d, x, y0, lane, Tp, R, m, p);
     else
         tile_words<SRC, NR, ZONES, false>(img, d, x, y0, lane, Tp, R, m, p);
-#ifdef IPP_CCL_DBG_MASK_ONLY  // diagnostic build (wrong output): the mask pass alone
-    if (lane == 0) k.tile[tile] = TileRec{0, -1, 0, 0};
-    if (m == 1ull) k.mask[0] = m;
-    return;
-#endif
     if (__ballot(m != 0ull) == 0ull) {  // no foreground: K2 and K6 skip the tile by its record
         if (lane == 0) k.tile[tile] = TileRec{0, -1, 0, 0};
         return;
@@ -656,7 +621,6 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
             cols[lane] = 0ull;
         }
         wave_sync();
-#ifndef IPP_CCL_DBG_NOSTATS
         for_runs(m, [&](int a, int len) {
             const int j = slot(r, a);
             const int v = par[pswz(j)];
@@ -668,9 +632,6 @@ k_ccl_label(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ 
                 if (v >= NJ) croot[c] = j;
             }
         });
-#else  // diagnostic build (wrong output): no per-component stats atomics
-        if (lane < MAXC) croot[lane] = slot(lane, 0);
-#endif
         wave_sync();
         const bool valid = lane < MAXC && c0 + lane < n;
         u64 cm = 0ull, rm = 0ull;
@@ -1054,10 +1015,7 @@ k_ccl_inwords(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __re
     k.mask[(int64_t)tile * TH + lane] = w;
 }
 
-#ifndef IPP_CCL_CROP_BLOCKS
-#define IPP_CCL_CROP_BLOCKS 256
-#endif
-constexpr int CROP_BLOCKS = IPP_CCL_CROP_BLOCKS;  // blocks per image striding over the crop
+constexpr int CROP_BLOCKS = 256;  // blocks per image striding over the crop
 
 __global__ void __launch_bounds__(256)
 k_ccl_crop_stream(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
@@ -1277,9 +1235,6 @@ extern "C" int ipp_video_keep_largest(const uint8_t* frames, const ipp_image_des
     const int rc =
         run_labels(SRC_HSV, frames, descs, n_images, max_w, max_h, hsv, works, scratch, counts, best, bbox, s, L);
     if (rc != IPP_OK) return rc;
-#if defined(IPP_CCL_DBG_NOSTATS) || defined(IPP_CCL_DBG_NOHSV) || defined(IPP_CCL_DBG_MASK_ONLY)
-    return IPP_OK;  // diagnostic builds: labelling only (their bboxes are not valid crops)
-#endif
     hipLaunchKernelGGL(k_ccl_inwords, L.group_grid, dim3(64 * WAVES), 0, s, descs, works, scratch, bbox,
                        L.groups_per_img, L.groups_x);
     hipLaunchKernelGGL(k_ccl_crop_stream, dim3((uint32_t)((int64_t)CROP_BLOCKS * n_images)), dim3(256), 0, s, frames,

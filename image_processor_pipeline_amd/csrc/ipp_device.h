@@ -129,23 +129,31 @@ __device__ __forceinline__ uint32_t clip8(int32_t ss) {
 // taking the low halves; 3 VALU instead of about 11.  In the pipe's H and V
 // epilogues: H launch 8.77 -> 8.64 ms (round 5, alternating runs on one box,
 // profiles/r05/ab_packed_clip_r05ao.txt).
-#ifndef IPP_PK_CLIP
-#define IPP_PK_CLIP 1
-#endif
+//
+// The compiler's hazard recognizer does not look inside inline asm, so an asm
+// operand written by an MFMA gets none of the wait states a VALU read of an
+// MFMA result needs: the inputs here must come from ordinary (compiler-seen)
+// instructions — planes3 below, or the shift of clip8x4_mfma.
 __device__ __forceinline__ uint32_t clip8x4(int32_t s0, int32_t s1, int32_t s2, int32_t s3) {
-#if IPP_PK_CLIP
     uint32_t lo, hi;
     asm("v_ashr_pk_u8_i32 %0, %1, %2, 22" : "=v"(lo) : "v"(s0), "v"(s1));
     asm("v_ashr_pk_u8_i32 %0, %1, %2, 22" : "=v"(hi) : "v"(s2), "v"(s3));
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
-#else
-    return clip8(s0) | (clip8(s1) << 8) | (clip8(s2) << 16) | (clip8(s3) << 24);
-#endif
+}
+
+// clip8x4 of four MFMA results: the >> 22 in plain code (hazard-checked),
+// then the packed saturation with shift 0.
+__device__ __forceinline__ uint32_t clip8x4_mfma(int32_t s0, int32_t s1, int32_t s2, int32_t s3) {
+    const int32_t v0 = s0 >> 22, v1 = s1 >> 22, v2 = s2 >> 22, v3 = s3 >> 22;
+    uint32_t lo, hi;
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 0" : "=v"(lo) : "v"(v0), "v"(v1));
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 0" : "=v"(hi) : "v"(v2), "v"(v3));
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
 // clip8x4(s) ^ 0x80808080 for s already lowered by 128 << 22 (folded into the
 // MFMA bias): clamp(v - 128, -128, 127) as a byte is clamp(v, 0, 255) ^ 0x80,
-// and v_ashr_pk_i8_i32 saturates to exactly that range.
+// and v_ashr_pk_i8_i32 saturates to exactly that range.  (Inputs: as clip8x4.)
 __device__ __forceinline__ uint32_t clip8x4_x80(int32_t s0, int32_t s1, int32_t s2, int32_t s3) {
     uint32_t lo, hi;
     asm("v_ashr_pk_i8_i32 %0, %1, %2, 22" : "=v"(lo) : "v"(s0), "v"(s1));
@@ -153,17 +161,15 @@ __device__ __forceinline__ uint32_t clip8x4_x80(int32_t s0, int32_t s1, int32_t 
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
-// a0 + (a1 << 8) + (a2 << 16) (the three tap byte planes' accumulators) in two
-// v_lshl_add_u32 (the compiler's form was two shifts and an add3).
+// a0 + (a1 << 8) + (a2 << 16) (the three tap byte planes' accumulators) as
+// ((a2 << 8) + a1 << 8) + a0: two v_lshl_add_u32 (left alone, the compiler
+// re-associates it into two shifts and an add3).  Plain code where it reads
+// the MFMA results, so they get their wait states (see clip8x4); the empty
+// asm only pins the intermediate (a VALU result).
 __device__ __forceinline__ int32_t planes3(int32_t a0, int32_t a1, int32_t a2) {
-#if IPP_PK_CLIP
-    int32_t t, r;
-    asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(t) : "v"(a1), "v"(a0));
-    asm("v_lshl_add_u32 %0, %1, 16, %2" : "=v"(r) : "v"(a2), "v"(t));
-    return r;
-#else
-    return a0 + (a1 << 8) + (a2 << 16);
-#endif
+    uint32_t t = ((uint32_t)a2 << 8) + (uint32_t)a1;
+    asm("" : "+v"(t));
+    return (int32_t)((t << 8) + (uint32_t)a0);
 }
 
 // Python slice(start, stop).indices(length) for step 1 (zone masks,
@@ -173,6 +179,30 @@ __device__ __forceinline__ void slice_indices(int start, int stop, int length, i
     if (stop < 0) { stop += length; if (stop < 0) stop = 0; } else if (stop > length) stop = length;
     lo = start;
     hi = stop < start ? start : stop;
+}
+
+// Division of block indices by a launch-invariant divisor without the ~30
+// instructions of a runtime integer division (a float reciprocal and two
+// fix-ups): q = umulhi(n, m) >> sh with m = ceil(2^(31 + l) / d), l =
+// ceil(log2 d), exact for every n < 2^31 (the error n·(m·d − 2^(31+l)) /
+// (d·2^(31+l)) stays below 1/d).  d = 1 is its own case (m would be 2^32).
+struct FastDiv {
+    uint32_t d, m, sh;
+};
+
+inline FastDiv fast_div(uint32_t d) {
+    FastDiv f{d, 0u, 0u};
+    if (d > 1) {
+        uint32_t l = 0;
+        while ((1ull << l) < d) ++l;
+        f.m = (uint32_t)(((1ull << (31 + l)) + d - 1) / d);
+        f.sh = l - 1;
+    }
+    return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    return f.d == 1u ? n : __umulhi(n, f.m) >> f.sh;
 }
 
 // XCD-aware block remap (cdna_hip_programming.md §5.5 T1): the dispatcher deals

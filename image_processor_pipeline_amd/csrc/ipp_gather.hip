@@ -32,10 +32,9 @@ struct TileGrid {
 //          a compact source patch — then each tile is restaged through LDS so
 //          every wave stores 4 full rows (256 B per row per instruction);
 //   ROWS:  wave w covers rows 4w..4w+3 directly (16 lanes × 4 pixels per row).
-#ifndef IPP_ROT_RT
-#define IPP_ROT_RT 2
-#endif
-constexpr int RT = IPP_ROT_RT;  // tiles per block (rows of 16)
+// Tiles per block: 1 / 2 / 4 measured 2.87 / 2.84 / 3.07 ms for config 2
+// (round 4, nontemporal stores).
+constexpr int RT = 2;  // tiles per block (rows of 16)
 
 template <int CN, bool PATCH, bool DENSE = false>
 __device__ __forceinline__ void rotate_tiles(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -115,16 +114,17 @@ __device__ __forceinline__ void rotate_tiles(const uint8_t* __restrict__ src, ui
     }
 }
 
+// (the block index split by FastDiv: the two runtime divisions were ~60 of
+// the kernel's ~350 scalar instructions)
 template <bool PATCH, bool DENSE = false>
 __global__ void __launch_bounds__(256)
 k_rotate_flip_nearest(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                      const ipp_gather_desc* __restrict__ descs, int tiles_x, int tiles_y) {
+                      const ipp_gather_desc* __restrict__ descs, FastDiv per_img, FastDiv tiles_x) {
     __shared__ uint4 stage[PATCH || DENSE ? TILE_H * (STAGE_W / 4) : 1];
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int per_img = tiles_x * tiles_y;
-    const int img = b / per_img;
-    const int t = b - img * per_img;
-    const int ty = t / tiles_x, tx = t - ty * tiles_x;
+    const int img = (int)fdiv(b, per_img);
+    const int t = (int)(b - (uint32_t)img * per_img.d);
+    const int ty = (int)fdiv((uint32_t)t, tiles_x), tx = t - ty * (int)tiles_x.d;
     const ipp_gather_desc d = descs[img];
     if (d.src_cn == 4) rotate_tiles<4, PATCH, DENSE>(src, dst, d, tx, ty, stage);  // block-uniform
     else rotate_tiles<3, PATCH, DENSE>(src, dst, d, tx, ty, stage);
@@ -261,23 +261,10 @@ extern "C" int ipp_rotate_flip_nearest(const uint8_t* src, uint8_t* dst, const i
     const int tx = (max_out_w + TILE_W - 1) / TILE_W, ty = (max_out_h + TILE_H * RT - 1) / (TILE_H * RT);
     const int64_t blocks = (int64_t)tx * ty * n_images;
     if (!grid_ok(blocks)) return IPP_E_ARG;
-#ifdef IPP_DIAG
-    static const int map = [] {  // experiment: 0 rows, 1 patch + LDS restage, 2 dense 8×8 + restage
-        const char* e = getenv("IPP_GATHER_MAP");
-        return e ? atoi(e) : 2;
-    }();
-#else
-    constexpr int map = 2;
-#endif
-    if (map == 0)
-        hipLaunchKernelGGL(k_rotate_flip_nearest<false>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
-                           src, dst, descs, tx, ty);
-    else if (map == 2)
-        hipLaunchKernelGGL((k_rotate_flip_nearest<false, true>), dim3((uint32_t)blocks), dim3(256), 0,
-                           (hipStream_t)stream, src, dst, descs, tx, ty);
-    else
-        hipLaunchKernelGGL(k_rotate_flip_nearest<true>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
-                           src, dst, descs, tx, ty);
+    // the dense 8×8 gather map with the LDS restage (the row map and the
+    // 16×16-patch map of rounds 1-2 measured slower)
+    hipLaunchKernelGGL((k_rotate_flip_nearest<false, true>), dim3((uint32_t)blocks), dim3(256), 0,
+                       (hipStream_t)stream, src, dst, descs, fast_div((uint32_t)(tx * ty)), fast_div((uint32_t)tx));
     IPP_CHECK_LAUNCH();
     return IPP_OK;
 }

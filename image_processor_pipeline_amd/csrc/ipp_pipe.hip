@@ -22,6 +22,11 @@
 // T (H-pass output) layout per item: [row group g][column x'][4 channels][4
 // rows] bytes (16 B per (g, x')), values XOR 0x80.  T rows are M rows
 // [line0, line0 + lines).
+//
+// Experiment switches left in this file are the live ones that DESIGN.md §3
+// names (IPP_HP_BANDS, IPP_COPY_GROUP/SLABS, IPP_VB_WPE/DB/HOIST_MAX); the
+// diagnostic builds of rounds 1-5 and the closed A/B switches were removed in
+// round 6 (their numbers stay in DESIGN.md).
 #include <algorithm>
 #include <type_traits>
 
@@ -30,19 +35,13 @@
 
 namespace {
 
-constexpr int HR = 16;            // H-pass rows per block (4 per thread)
+constexpr int HR = 16;            // H-pass rows per band (4 per thread)
 constexpr int RING = 512;         // window ring: M columns x live at x & (RING - 1)
 // LDS bytes per plane row of the window ring.  544 ≡ 8 dwords mod 64 banks:
 // the phase-2 ds_read_b128 (4 lane groups of 16, 4 dwords each) then covers
 // 64 distinct banks per group, and the phase-1 ds_write_b32 rows pair up 2-way,
 // which a dword store absorbs (MI355X_MICROARCH.md §LDS).
 constexpr int WSTRIDE = 544;
-#ifdef IPP_DIAG
-inline int diag_env(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-#endif
 
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
     return __builtin_amdgcn_perm(hi, lo, sel);
@@ -58,38 +57,11 @@ __device__ __forceinline__ void transpose4(uint32_t p0, uint32_t p1, uint32_t p2
     ch[3] = perm(hi23, hi01, 0x07060302u);
 }
 
-// Q22 lane pair (dx = lane & 1) holding columns {dx, dx + 2, dx + 4, dx + 6}
-// of one row → lane 0 holds columns 0..3, lane 1 columns 4..7 (two DPP
-// swaps with the partner lane).
-__device__ __forceinline__ void pair_regroup(uint32_t (&a)[4], bool o1) {
-    const uint32_t s0 = o1 ? a[0] : a[2], s1 = o1 ? a[1] : a[3];
-    const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s0, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
-    const uint32_t r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0xB1, 0xF, 0xF, false);
-    const uint32_t b0 = o1 ? r0 : a[0], b1 = o1 ? a[2] : r0, b2 = o1 ? r1 : a[1], b3 = o1 ? a[3] : r1;
-    a[0] = b0;
-    a[1] = b1;
-    a[2] = b2;
-    a[3] = b3;
-}
-
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-// Cache policy of the background copy's loads (experiment switch; 0 = plain
-// loads, 16 = sc1: served by L2, not kept in the CU's L1, which the gathers
-// need).
-#ifndef IPP_COPY_POL
-#define IPP_COPY_POL 0
-#endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFFF, 0x00020000);
-}
-__device__ __forceinline__ uint4 ld_tap(const uint4* base, int idx) {
-#if defined(IPP_DIAG) && defined(IPP_DIAG_NOTAPS)
-    // diagnostic (wrong output): no tap loads, constant operands
-    { const uint32_t v = (uint32_t)idx * 0x01010101u; asm volatile("" :: "v"(v)); return make_uint4(v, v ^ 1u, v ^ 2u, v ^ 3u); }
-#endif
-    return base[idx];
 }
 
 // ---------------------------------------------------------------------------
@@ -107,10 +79,10 @@ __device__ __forceinline__ uint4 ld_tap(const uint4* base, int idx) {
 //
 // Block = one 16-row band of one item, 4 waves.  It sweeps the item's output
 // tiles in chunks of ≤ 4 tiles whose input window fits the 512-column
-// channel-planar LDS ring.  Phase 1 gathers the chunk's new M columns into
-// the ring (16 columns × 16 rows per wave and step; a lane takes 4
-// consecutive M columns of one row, i.e. the ring dword it writes); phase 2
-// runs the taps on the matrix cores.
+// channel-planar LDS ring.  Phase 1 gathers the chunk's new M columns into the
+// ring (16 columns × 16 rows per wave and step; a lane takes 4 consecutive M
+// columns of one row, i.e. the ring dword it writes); phase 2 runs the taps on
+// the matrix cores.
 // (An LDS-staged form — coalesced source spans, dense HSV — was bit-exact but
 // 1.6× slower, VALU-bound: DESIGN.md §3, profiles/r03_staged/.)
 // ---------------------------------------------------------------------------
@@ -119,16 +91,13 @@ typedef uint8_t WinRing[4][HR][WSTRIDE];   // planar window ring, bytes p ^ 0x80
 template <int NR>
 struct __attribute__((aligned(16))) Hpass2Lds {
     WinRing win;
-    HsvTables<NR> T;               // table-driven HSV test (ipp_hsv.h)
+    HsvTables<NR> T;                  // table-driven HSV test (ipp_hsv.h)
     int32_t zc[NR > 8 ? 2 * NR : 1];  // > 8 ranges with zones: column bounds here, not in registers
 };
 
 // M pixel → window byte quad (p | α 255) ^ 0x80 when kept, 0x80808080 (transparent black) when excluded.
 template <int NR, bool ZONES>
 __device__ __forceinline__ uint32_t hsv2_px(const HsvTables<NR>& T, uint32_t raw, uint32_t zbits) {
-#if defined(IPP_DIAG) && defined(IPP_DIAG_NOHSV)
-    return ((raw | 0xFF000000u) ^ 0x80808080u) & (zbits | 0xFFFFFF00u);  // diagnostic (wrong output): no HSV test
-#endif
     uint32_t ex = hsv_tab_excl<NR, false>(T, raw);
     if (ZONES) ex &= zbits;
     const uint32_t t = (raw | 0xFF000000u) ^ 0x80808080u;
@@ -137,7 +106,7 @@ __device__ __forceinline__ uint32_t hsv2_px(const HsvTables<NR>& T, uint32_t raw
 
 // Per-block state.
 struct Hp2Block {
-    u32x4_t rsv;                // source window buffer resource (records = bytes to the image end)
+    u32x4_t rsv;                // source window buffer resource
     uint32_t lim;               // CLAMP: last byte offset where a dword fits
     uint32_t rowx, rowy;        // 16.16 source position of column 0 of the lane's row
     int32_t b0, b3, pitch, in_w, in_h;
@@ -189,18 +158,6 @@ __device__ __forceinline__ void asm_wait(uint32_t (&p)[4], int32_t newer) {
         "s_waitcnt vmcnt(4)\n\t"
         "s_branch 4f\n"
         "2:\n\t"
-#if defined(IPP_DIAG) && defined(IPP_DIAG_X3)
-        "s_cmp_eq_u32 %4, 2\n\t"
-        "s_cbranch_scc0 3f\n\t"
-        "s_waitcnt vmcnt(2)\n\t"
-        "s_branch 4f\n"
-        "3:\n\t"
-        "s_cmp_eq_u32 %4, 1\n\t"
-        "s_cbranch_scc0 5f\n\t"
-        "s_waitcnt vmcnt(1)\n\t"
-        "s_branch 4f\n"
-        "5:\n\t"
-#endif
         "s_cmp_eq_u32 %4, 0\n\t"
         "s_cbranch_scc0 4f\n\t"
         "s_waitcnt vmcnt(0)\n"
@@ -210,31 +167,18 @@ __device__ __forceinline__ void asm_wait(uint32_t (&p)[4], int32_t newer) {
         : "scc");
 }
 
-// H-pass T bytes by signed saturation of bias-lowered sums (clip8x4_x80).
-#ifndef IPP_PK_T
-#define IPP_PK_T 1
-#endif
-
-// A lane's four pixels of a step: 4 consecutive M columns (IPP_HP_CONSEC, the
-// ring's dword as gathered), or columns 2 apart with the partner lane holding
-// the others (a lane quad = a 2×2 block of M pixels; pair_regroup then swaps
-// them into consecutive columns).
-// Consecutive columns: no pair exchange (2 VALU per pixel), H launch
-// 8.79-8.81 -> 8.74-8.76 ms (round 5, alternating runs on one box,
-// profiles/r05/ab_gather_consec_r05aj.txt).
-// Gathers: the row test by the buffer's range check (H 8.79 -> 8.75 ms,
-// round 5, alternating runs on one box, profiles/r05/ab_gather_yrange_r05ar.txt).
-#ifndef IPP_HP_YRANGE
-#define IPP_HP_YRANGE 1
-#endif
-#ifndef IPP_HP_CONSEC
-#define IPP_HP_CONSEC 1
-#endif
-constexpr int kPixStep = IPP_HP_CONSEC ? 1 : 2;
-
 // Gathers of one live step: xx/yy = 16.16 source position of the lane's
-// first pixel (its next three are kPixStep columns apart).  Out-of-window pixels load
-// offset 0xFFFFFFFF (the range check returns 0).
+// first pixel (its next three are the following M columns).  Out-of-window
+// pixels load offset 0xFFFFFFFF (the range check returns 0).  Two forms:
+//   CLAMP (general): column and row tested, the records run to the image end,
+//   and an offset past the last whole dword is clamped back (the pixel then
+//   loaded one byte early, fl);
+//   fast (the bench's crops): rows outside the window fail the buffer's range
+//   check by themselves — the records end one byte past the window's last
+//   pixel and row in_h starts at or past that byte — so only the column is
+//   tested (H 8.79 -> 8.75 ms, round 5, profiles/r05/ab_gather_yrange_r05ar.txt);
+//   hpass_block takes it only where that holds and no row offset can wrap
+//   (yr_range_ok).
 template <int CN, bool CLAMP>
 __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32_t yy, Raw4& o) {
     bool any = false;
@@ -243,12 +187,8 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int xin = (int32_t)xx >> 16, yin = (int32_t)yy >> 16;
-        // (IPP_HP_YRANGE: rows outside the window fail the buffer's range
-        // check by themselves — its records end one byte past the window's
-        // last pixel — so only the column is tested; not under CLAMP, whose
-        // offsets are clamped back into range)
-        const bool ok = IPP_HP_YRANGE && !CLAMP ? (uint32_t)xin < (uint32_t)B.in_w
-                                      : ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h);
+        const bool ok = CLAMP ? ((uint32_t)xin < (uint32_t)B.in_w) & ((uint32_t)yin < (uint32_t)B.in_h)
+                              : (uint32_t)xin < (uint32_t)B.in_w;
         uint32_t o1 = (uint32_t)__mul24(yin, B.pitch) + (uint32_t)__umul24((uint32_t)xin, (uint32_t)CN);
         if (CLAMP) {
             const uint32_t offc = min(o1, B.lim);
@@ -256,51 +196,17 @@ __device__ __forceinline__ void hp2_issue(const Hp2Block& B, uint32_t xx, uint32
             o1 = offc;
         }
         off[k] = ok ? o1 : 0xFFFFFFFFu;
-#if defined(IPP_DIAG) && defined(IPP_DIAG_ALIGNED)
-        off[k] = ok ? (o1 & ~3u) : 0xFFFFFFFFu;  // diagnostic (wrong output): dword-aligned gathers
-#endif
         any |= ok;
-        xx += (uint32_t)(kPixStep * B.b0);
-        yy += (uint32_t)(kPixStep * B.b3);
+        xx += (uint32_t)B.b0;
+        yy += (uint32_t)B.b3;
     }
-#if defined(IPP_DIAG) && defined(IPP_DIAG_NOGATHER)
-    // diagnostic (wrong output): no gathers, pixel values from the offsets
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { o.p[k] = off[k] * 0x9E3779B1u; asm volatile("" : "+v"(o.p[k])); }
-#elif defined(IPP_DIAG) && defined(IPP_DIAG_X3)
-    // diagnostic (wrong output): one 12-byte load at the lane's first pixel
-    {
-        typedef uint32_t u32x3v __attribute__((ext_vector_type(3)));
-        u32x3v v;
-        asm volatile("buffer_load_dwordx3 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off[0]), "s"(B.rsv));
-        o.p[0] = v.x;
-        o.p[1] = v.y;
-        o.p[2] = v.z;
-        o.p[3] = v.x;
-    }
-#elif defined(IPP_DIAG) && defined(IPP_DIAG_GATHER_L1)
-    // diagnostic (wrong output): the same gathers folded into a 16 KB window
-#pragma unroll
-    for (int k = 0; k < 4; ++k) o.p[k] = asm_gather(B.rsv, off[k] == 0xFFFFFFFFu ? off[k] : (off[k] & 0x3FFFu));
-#else
 #pragma unroll
     for (int k = 0; k < 4; ++k) o.p[k] = asm_gather(B.rsv, off[k]);
-#endif
     o.any = any;
     o.live = true;
 }
 
-#if defined(IPP_DIAG) && defined(IPP_DIAG_X3)
-constexpr int kLoadsPerSet = 1;  // diagnostic (wrong output): one 12-byte load per lane and step
-#else
-constexpr int kLoadsPerSet = 4;
-#endif
-constexpr int HP_NW = 4;              // waves per block (one 16-row band)
-#if defined(IPP_DIAG) && defined(IPP_DIAG_NOSYNC)
-#define IPP_HP_SYNC() ((void)0)  // diagnostic (wrong output): no chunk barriers
-#else
-#define IPP_HP_SYNC() __syncthreads()
-#endif
+constexpr int HP_NW = 4;              // waves per block
 constexpr int HP_STEPC = 16 * HP_NW;  // M columns per block-wide phase-1 step
 
 // Sticky status of the pipe kernels (ipp_pipe_status): bit 0 = an H-pass
@@ -336,35 +242,28 @@ __device__ __forceinline__ Hp2Chunk hp2_chunk(const int4* hdr, int s0, int ntile
     return c;
 }
 
+// (Round 6: a block walking 2-4 bands chunk-outer, band-inner — each chunk's
+// taps loaded once for its bands, its window re-gathered per band — measured
+// slower than this one-band block: the taps, meta and bias held across the
+// next band's phase 1 cost more than the tap loads they save; DESIGN.md §3
+// "Round 6, multi-band H blocks".)
 template <int NR, bool ZONES, int CN, bool CLAMP>
 __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win, int wave, const Hp2Block& B,
-                                            uint8_t* __restrict__ tmp,
-                                            const int32_t* __restrict__ coefs, const ipp_resample_desc& h,
-                                            int row0, int nrows, const int32_t* zc0, const int32_t* zcw,
-                                            uint32_t zrow, uint32_t fill) {
+                                            uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
+                                            const ipp_resample_desc& h, int row0, int nrows, const int32_t* zc0,
+                                            const int32_t* zcw, uint32_t zrow, uint32_t fill) {
     const int lane = threadIdx.x & 63;
     const int r = 2 * (lane >> 3) + ((lane >> 1) & 1);  // the lane's window row
     const int ntiles = (h.out_len + 15) >> 4;
     const int4* hdr = reinterpret_cast<const int4*>(coefs + h.coef_off);
     const int32_t* tbias = coefs + h.coef_off + 4 * (int64_t)ntiles;
     const uint4* tblk = reinterpret_cast<const uint4*>(coefs + h.coef_off + 20 * (int64_t)ntiles);
-#if defined(IPP_DIAG) && defined(IPP_DIAG_TAPSHARE)
-    // diagnostic (wrong output): every block's tap loads read the first item's
-    // blocks (same instructions, L1/L2-resident lines)
-    const uint4* tblk_d = reinterpret_cast<const uint4*>(coefs + 20 * (int64_t)ntiles);
-#define IPP_TAP_INDEX(i) (((i) & 1023))
-#else
-#define IPP_TAP_INDEX(i) (i)
-    const uint4* tblk_d = tblk;
-#endif
     const uint32_t sx = (uint32_t)HP_STEPC * (uint32_t)B.b0, sy = (uint32_t)HP_STEPC * (uint32_t)B.b3;  // per-step advance
 
     int filled = hdr[0].x;  // ring holds M columns [.., filled)
     Hp2Chunk ck = hp2_chunk(hdr, 0, ntiles, filled, wave);
     // Lane's first column of step 0 and its source position.
-    auto lane_x = [&](const Hp2Chunk& c) {
-        return c.c0 + 16 * wave + 8 * ((lane >> 2) & 1) + (IPP_HP_CONSEC ? 4 : 1) * (lane & 1);
-    };
+    auto lane_x = [&](const Hp2Chunk& c) { return c.c0 + 16 * wave + 8 * ((lane >> 2) & 1) + 4 * (lane & 1); };
     // (24-bit products: columns < 2^15 and |b| ≤ 2^16; a 32-bit product made
     // the compiler use a 64-bit mad whose unused high addend was a register
     // that can still be in flight)
@@ -411,7 +310,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             // per plane — one load per plane for every K step.  Dense tiles:
             // the first K step's blocks (meta then reads tap bytes, unused).
 #pragma unroll
-            for (int p = 0; p < 3; ++p) bn[p] = ld_tap(tblk_d, IPP_TAP_INDEX(th.z + (th.w ? 4 : 0) + lane + p * 64));
+            for (int p = 0; p < 3; ++p) bn[p] = tblk[th.z + (th.w ? 4 : 0) + lane + p * 64];
             if (!has_tile) th.y = 0;
         }
         const int te = min(t, ntiles - 1);
@@ -422,8 +321,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // newer = gather loads issued after P's (4 per live later set)
         auto process = [&](Raw4& P, int st, int newer) {
             asm_wait(P.p, P.live ? newer : -1);
-            // lane dx holds columns 8gc + 4dx .. +3 (after the pair exchange
-            // when the pixels are 2 columns apart)
+            // lane holds columns 8gc + 4dx .. +3 of its row
             const int cg = wave * 4 + 4 * HP_NW * st + 2 * ((lane >> 2) & 1) + (lane & 1);
             const int x = c0 + 4 * cg;
             const bool active = (cg < ng4) && (r < nrows);
@@ -432,9 +330,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             for (int k = 0; k < 4; ++k) {
                 zb[k] = ~0u;
                 if (ZONES) {
-                    // column of gather k's pixel (before the pair exchange)
-                    const int xk = c0 + 16 * wave + HP_STEPC * st + 8 * ((lane >> 2) & 1) +
-                                   (IPP_HP_CONSEC ? 4 : 1) * (lane & 1) + kPixStep * k;
+                    const int xk = x + k;
                     zb[k] = 0;
 #pragma unroll
                     for (int q = 0; q < NR; ++q) zb[k] |= (uint32_t)((uint32_t)(xk - zc0[q]) < (uint32_t)zcw[q]) << q;
@@ -451,12 +347,10 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                     if (CLAMP) raw >>= ((P.fl >> (1 + k)) & 1u) << 3;
                     px[k] = hsv2_px<NR, ZONES>(T, raw, zb[k]);
                 }
-                if (!IPP_HP_CONSEC) pair_regroup(px, lane & 1);
                 transpose4(px[0], px[1], px[2], px[3], ch);
             } else if (ZONES) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) px[k] = hsv2_px<NR, ZONES>(T, 0u, zb[k]);
-                if (!IPP_HP_CONSEC) pair_regroup(px, lane & 1);
                 transpose4(px[0], px[1], px[2], px[3], ch);
             } else {
 #pragma unroll
@@ -475,11 +369,11 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // copies, and copying a register whose load is in flight waits for it.
         for (int st = 0; st < nsteps; st += 3) {
             iss(st + 2, RC);
-            process(RA, st, kLoadsPerSet * (RB.live + RC.live));
+            process(RA, st, 4 * (RB.live + RC.live));
             iss(st + 3, RA);
-            process(RB, st + 1, kLoadsPerSet * (RC.live + RA.live));
+            process(RB, st + 1, 4 * (RC.live + RA.live));
             iss(st + 4, RB);
-            process(RC, st + 2, kLoadsPerSet * (RA.live + RB.live));
+            process(RC, st + 2, 4 * (RA.live + RB.live));
         }
 
         // The chunk's first tap loads (issued before its gathers) and the bias
@@ -510,20 +404,18 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // registers and broke parity.)
         issue(ck, 0, xxl, yyl, RA);
         issue(ck, 1, xxl + sx, yyl + sy, RB);
-        IPP_HP_SYNC();
+        __syncthreads();
 
         // Phase 2 (mfma): wave w takes tile s0 + w; A = 16 window rows × 64
         // columns of one channel (lane l: row l&15, bytes 16(l>>4)..+15),
         // B = 64 columns × 16 outputs of one tap byte plane.  D lane l =
         // output l&15, rows 4(l>>4)..+3 = exactly one 16-B T group.  The
-        // column bias rides in the first byte plane's initial accumulator.
-#if defined(IPP_DIAG) && defined(IPP_DIAG_NOPH2)
-        if (has_tile && nrows < 0) {  // diagnostic (wrong output): no MFMA phase
-#else
+        // column bias (lowered by 128 << 22, so that the signed saturation
+        // below yields clip8 ^ 0x80) rides in the first byte plane's initial
+        // accumulator.
         if (has_tile) {
-#endif
             i32x4 acc[4][3];
-            const int32_t b0 = IPP_PK_T ? bias - (128 << 22) : bias;
+            const int32_t b0 = bias - (128 << 22);
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 acc[c][0] = i32x4{b0, b0, b0, b0};
@@ -565,12 +457,7 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
                 for (int ks = 0; ks < th.y; ++ks) {
                     if (ks > 0) {
 #pragma unroll
-                        for (int p = 0; p < 3; ++p) {
-#if defined(IPP_DIAG) && defined(IPP_DIAG_TAPHALF)
-                            if (ks < 2) continue;  // diagnostic (wrong output): K step 1 reuses step 0's taps
-#endif
-                            bn[p] = ld_tap(tblk_d, IPP_TAP_INDEX(th.z + lane + (ks * 3 + p) * 64));
-                        }
+                        for (int p = 0; p < 3; ++p) bn[p] = tblk[th.z + lane + (ks * 3 + p) * 64];
                     }
                     const int pos = (th.x + 64 * ks + akoff) & (RING - 1);
 #pragma unroll
@@ -585,17 +472,15 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
             }
             const int xo = 16 * t + (lane & 15);
             if (xo < h.out_len) {
-                // T bytes = clip8 ^ 0x80 (the MFMA's signed form); with
-                // IPP_PK_T the ^ 0x80 comes from the signed saturation of
-                // sums lowered by 128 << 22 in the bias (acc init above)
+                // T bytes = clip8 ^ 0x80 (the MFMA's signed form), from the
+                // signed saturation of the bias-lowered sums
                 uint32_t outc[4];
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     int32_t ss[4];
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr) ss[rr] = planes3(acc[c][0][rr], acc[c][1][rr], acc[c][2][rr]);
-                    outc[c] = IPP_PK_T ? clip8x4_x80(ss[0], ss[1], ss[2], ss[3])
-                                       : clip8x4(ss[0], ss[1], ss[2], ss[3]) ^ 0x80808080u;
+                    outc[c] = clip8x4_x80(ss[0], ss[1], ss[2], ss[3]);
                 }
                 // (an opaque lane copy: hoisted out of the chunk loop, this
                 // 64-bit row address was live through phase 1 and spilled)
@@ -613,24 +498,17 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // The next chunk's first sets are waited for here, at the end of
         // phase 2 (which hid their latency): from this point on the compiler
         // may copy their registers (it does, at the loop's back edge).
-#if defined(IPP_DIAG) && defined(IPP_DIAG_X3)
-        asm_wait(RA.p, RA.live ? kLoadsPerSet * RB.live : -1);
-        asm_wait(RB.p, RB.live ? 0 : -1);
-        if (!more) break;
-#else
         asm_wait(RA.p, RA.live ? 4 * RB.live : -1);
         asm_wait(RB.p, RB.live ? 0 : -1);
         if (!more) break;
-#endif
-        IPP_HP_SYNC();
+        __syncthreads();
     }
 }
 
 // Composite rows outside the overlay's 16-row bands [vb0, vb1) are plain
 // copies of the background (Paste.c leaves them untouched).  The H-pass
-// blocks of an item share that copy (block `share` of `nshare`): it rides on a
-// memory system the VALU-bound H pass leaves idle, and ipp_pipe_vblend_bands
-// then only visits the bands the overlay touches.
+// launch's copy blocks write them (and, column split, the band rows' groups
+// outside the overlay), so ipp_pipe_vblend_bands only visits the overlay.
 __device__ __forceinline__ void paste_bands(const ipp_paste_desc& p, int& vb0, int& vb1) {
     vb0 = (p.y >> 4) << 4;
     vb1 = min(p.bg_h, ((p.y + p.ov_h + 15) >> 4) << 4);
@@ -642,28 +520,23 @@ __device__ __forceinline__ void paste_bands(const ipp_paste_desc& p, int& vb0, i
 // band rows' 16-pixel groups outside [gx0, gx1) (the groups the overlay
 // touches) and the V pass visits only [gx0, gx1).  Both kernels decide it
 // with this one predicate (ipp_plan.cpp counts the bytes the same way).
-#ifndef IPP_BAND_SPLIT
-#define IPP_BAND_SPLIT 1  // (0: experiment builds, the V pass copies whole band rows)
-#endif
 __device__ __forceinline__ bool band_cols_split(const ipp_paste_desc& p, const uint8_t* bg, const uint8_t* dst,
                                                 int& gx0, int& gx1) {
     const int rb = 3 * p.bg_w;
     gx0 = max(p.x, 0) >> 4;
     gx1 = min((p.x + p.ov_w + 15) >> 4, p.bg_w >> 4);
     const int64_t lr = 3 * (p.bg_w >> 4);  // ≥ the split's vectors per band row
-    return IPP_BAND_SPLIT && (p.bg_w & 15) == 0 && p.bg_pitch == rb && p.dst_pitch == rb && gx0 < gx1 &&
+    return (p.bg_w & 15) == 0 && p.bg_pitch == rb && p.dst_pitch == rb && gx0 < gx1 &&
            (int64_t)p.bg_h * lr * lr < (1ll << 32) &&  // (the H copy's umulhi division stays exact)
            ((reinterpret_cast<uintptr_t>(bg + p.bg_off) | reinterpret_cast<uintptr_t>(dst + p.dst_off)) & 15u) == 0;
 }
 
-// 16-B vectors per thread in flight in the background copy (IPP_COPY_U
-// overrides it in experiment builds).  A copy block holds one of the CU's
-// four H-pass block slots for as long as it streams, so bytes in flight per
-// block set how much H-pass time the copy displaces.
-#ifndef IPP_COPY_U
-#define IPP_COPY_U 16
-#endif
-template <int NT = 256, int U = IPP_COPY_U>
+// 16-B vectors per thread in flight in the per-item background copy.  A copy
+// block holds one of the CU's four H-pass block slots for as long as it
+// streams, so bytes in flight per block set how much H-pass time the copy
+// displaces.
+constexpr int kCopyU = 16;
+template <int NT = 256, int U = kCopyU>
 __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, const uint8_t* __restrict__ bg,
                                                       uint8_t* __restrict__ dst, int share, int nshare) {
     int vb0, vb1;
@@ -689,24 +562,19 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
         auto vec_of = [&](int64_t i) -> int64_t {
             if (i < n0) return i;
             if (i < n0 + n1) return i + skip;
-            const uint32_t j = (uint32_t)(i - n0 - n1);   // j·LR < 2^32: umulhi exact
+            // j < n2 ≤ bg_h·LR, so j·LR < 2^32 (band_cols_split) and umulhi is exact
+            const uint32_t j = (uint32_t)(i - n0 - n1);
             const uint32_t r = __umulhi(j, mag), c = j - r * (uint32_t)LR;
             return (int64_t)(vb0 + (int)r) * rv + (int)c + ((int)c < L ? 0 : rgt);
         };
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4* s4 = reinterpret_cast<const u32x4*>(sb);
-        u32x4* d4 = reinterpret_cast<u32x4*>(db);
-        const __amdgpu_buffer_rsrc_t srs = rsrc_of(sb);
+        const u32x4_t* s4 = reinterpret_cast<const u32x4_t*>(sb);
+        u32x4_t* d4 = reinterpret_cast<u32x4_t*>(db);
         for (int64_t i0 = a + threadIdx.x; i0 < e; i0 += U * NT) {
-            u32x4 v[U];
+            u32x4_t v[U];
 #pragma unroll
             for (int j = 0; j < U; ++j) {
                 const int64_t i = i0 + NT * j;
-                if (i < e) {
-                    const int64_t k = vec_of(i);
-                    if (IPP_COPY_POL == 0) v[j] = s4[k];
-                    else v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, (uint32_t)k * 16u, 0, IPP_COPY_POL));
-                }
+                if (i < e) v[j] = s4[vec_of(i)];
             }
 #pragma unroll
             for (int j = 0; j < U; ++j) {
@@ -756,17 +624,10 @@ __device__ __forceinline__ void bg_copy_outside_bands(const ipp_paste_desc& p, c
 #define IPP_COPY_SLABS IPP_COPY_GROUP
 #endif
 // 16-B vectors per thread in flight in the grouped copy (8 made the kernel
-// spill inside the H pass's 128-VGPR budget; 2 measured 0.5 % slower than 4)
-#ifndef IPP_COPY_GU
-#define IPP_COPY_GU 4
-#endif
-// Store form of the grouped copy: 0 = global nontemporal store, 1 = plain,
-// else a buffer store with these cache-policy bits.  B = 4096, one box,
-// alternating: 9.02-9.03 (0) / 9.35 (1) / 8.98-9.00 (2: nt) / 8.98-9.00 (3:
-// sc0 nt) / 9.41 (16: sc1) / 9.07 (18: sc1 nt) ms for the H launch.
-#ifndef IPP_COPY_STPOL
-#define IPP_COPY_STPOL 2
-#endif
+// spill inside the H pass's 128-VGPR budget; 2 measured 0.5 % slower than 4).
+// Stores: buffer stores with the nt bit (global nt stores 9.02-9.03, plain
+// 9.35, sc1 9.41 ms for the H launch; round 5, one box).
+constexpr int kCopyGU = 4;
 constexpr int kCopyGroup = IPP_COPY_GROUP;  // items per copy group (≤ 64: one lane per item)
 constexpr int kCopySlabs = IPP_COPY_SLABS;  // copy blocks (row slabs) per group
 static_assert(kCopyGroup >= 1 && kCopyGroup <= 64, "one lane per item of a copy group");
@@ -781,7 +642,7 @@ struct CopyItem {
     int32_t flat;             // composite is a flat 16-B aligned copy of bg
 };
 
-template <int NT = 256, int U = IPP_COPY_GU>
+template <int NT = 256, int U = kCopyGU>
 __device__ __forceinline__ void bg_copy_group(const ipp_pipe_desc* __restrict__ descs, int n, int i0, int slab,
                                               const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst) {
     const int cnt = min(kCopyGroup, n - i0);
@@ -806,9 +667,12 @@ __device__ __forceinline__ void bg_copy_group(const ipp_pipe_desc* __restrict__ 
         const bool split = band_cols_split(p, bg, dst, gx0, gx1);
         ci.c0 = split ? 3 * gx0 : 0;
         ci.c1 = split ? 3 * gx1 : rb / 16;
+        // The slab's vector index i is split into (row, column) by umulhi(i,
+        // ⌈2^32 / rv⌉), exact while i·rv < 2^32: the slab's vector count times
+        // rv must stay below 2^32 (and row / column fit 16 bits each).
+        const int64_t rv = rb / 16, slab_rows = (p.bg_h + kCopySlabs - 1) / kCopySlabs;
         ci.flat = p.bg_pitch == rb && p.dst_pitch == rb && (rb & 15) == 0 && ((du | bu) & 15u) == 0 &&
-                  p.bg_w < 65536 && p.bg_h < 32768 &&
-                  (int64_t)((p.bg_h + kCopySlabs - 1) / kCopySlabs) * (rb / 16) < (1 << 24);  // umulhi exact
+                  p.bg_w < 65536 && p.bg_h < 32768 && slab_rows * rv * rv < (1ll << 32);
     }
     auto rl = [](int32_t v, int j) { return __builtin_amdgcn_readlane(v, j); };
     auto rlu = [](uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int32_t)v, j); };
@@ -827,11 +691,10 @@ __device__ __forceinline__ void bg_copy_group(const ipp_pipe_desc* __restrict__ 
             const int rv = 3 * bw / 16;  // vectors per row
             const int ya = (int)((int64_t)bh * slab / kCopySlabs), ye = (int)((int64_t)bh * (slab + 1) / kCopySlabs);
             const uint32_t total = (uint32_t)((ye - ya) * rv);
-            const uint32_t mag = (uint32_t)((0x100000000ull + rv - 1) / rv);  // i / rv = umulhi(i, mag), i < 2^24
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4* s4 = reinterpret_cast<const u32x4*>(((uint64_t)bhi << 32) | blo) + (int64_t)ya * rv;
+            const uint32_t mag = (uint32_t)((0x100000000ull + rv - 1) / rv);  // i / rv = umulhi(i, mag) for i·rv < 2^32
+            const u32x4_t* s4 = reinterpret_cast<const u32x4_t*>(((uint64_t)bhi << 32) | blo) + (int64_t)ya * rv;
             for (uint32_t ib = threadIdx.x; ib < total; ib += U * NT) {
-                u32x4 v[U];
+                u32x4_t v[U];
                 uint32_t rc[U];  // slab row << 16 | vector column (one register per vector)
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -845,22 +708,14 @@ __device__ __forceinline__ void bg_copy_group(const ipp_pipe_desc* __restrict__ 
                     // the item's band rows relative to the slab, its band-row vectors [c0, c1)
                     const int32_t r0 = rl(ci.vb0, j) - ya, rn = rl(ci.vb1, j) - rl(ci.vb0, j);
                     const int32_t c0 = rl(ci.c0, j), cn = rl(ci.c1, j) - c0;
-                    u32x4* d4 = reinterpret_cast<u32x4*>(((uint64_t)rlu(ci.dhi, j) << 32) | rlu(ci.dlo, j)) +
-                                (int64_t)ya * rv;
+                    u32x4_t* d4 = reinterpret_cast<u32x4_t*>(((uint64_t)rlu(ci.dhi, j) << 32) | rlu(ci.dlo, j)) +
+                                  (int64_t)ya * rv;
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const uint32_t i = ib + NT * u;
                         const bool inside = (uint32_t)((int32_t)(rc[u] >> 16) - r0) < (uint32_t)rn &&
                                             (uint32_t)((int32_t)(rc[u] & 0xFFFFu) - c0) < (uint32_t)cn;
-                        if (i < total && !inside) {
-#if IPP_COPY_STPOL == 0
-                            __builtin_nontemporal_store(v[u], d4 + i);
-#elif IPP_COPY_STPOL == 1
-                            d4[i] = v[u];
-#else
-                            __builtin_amdgcn_raw_buffer_store_b128(v[u], rsrc_of(d4), i * 16u, 0, IPP_COPY_STPOL);
-#endif
-                        }
+                        if (i < total && !inside) __builtin_amdgcn_raw_buffer_store_b128(v[u], rsrc_of(d4), i * 16u, 0, 2);
                     }
                 }
             }
@@ -870,6 +725,15 @@ __device__ __forceinline__ void bg_copy_group(const ipp_pipe_desc* __restrict__ 
             if (!((fm >> j) & 1u)) bg_copy_outside_bands<NT>(descs[i0 + j].p, bg, dst, slab, kCopySlabs);
         j0 = j1;
     }
+}
+
+// May an H-pass block of this window drop the gathers' row test (YR)?  Row
+// in_h must start at or past the buffer's last record (need), and no row
+// offset yin·pitch (|yin| ≤ 2^15: 16.16 positions) may wrap around 2^32 back
+// into [0, need).  (A full-width crop of a dense 3-channel source, pitch =
+// 3·in_w, has in_h·pitch = need - 1 and keeps the row test.)
+__device__ __forceinline__ bool yr_range_ok(int in_h, int pitch, int need) {
+    return (int64_t)in_h * pitch >= (int64_t)need && (int64_t)32768 * pitch + need <= (int64_t)1 << 32;
 }
 
 // One H-pass block: band tb of item im.
@@ -885,16 +749,6 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
     hsv_tables_init<NR>(L.T, hp);
-#if defined(IPP_DIAG) && defined(IPP_DIAG_SETUP2)
-    // diagnostic: the block set-up twice (its cost)
-    __syncthreads();
-    {
-        ipp_hsv_params hq = hp;
-        asm volatile("" : "+v"(hq.r[0].lo[0]));
-        hsv_tables_init<NR>(L.T, hq);
-        __syncthreads();
-    }
-#endif
 
     // Zones: per-lane row bits now, column bits per pixel.  With > 8 ranges
     // the column bounds live in LDS (in registers they spilled).
@@ -929,14 +783,16 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
     // buffer load into a waterfall loop; items are < 2 GiB, checked on the host.)
     const int nrec = (g.src_h - g.in_y0) * g.src_pitch - g.in_x0 * g.src_cn;
     const int need = (g.in_h - 1) * g.src_pitch + g.in_w * CN + (CN == 3 ? 1 : 0);
-    const bool clamp = need > nrec;  // last pixel's dword would cross the image end (block-uniform)
+    // The fast body needs no clamp (the last pixel's dword ends inside the
+    // image) and a window whose rows the range check can reject; every other
+    // block takes the general (CLAMP) body.  Block-uniform.
+    const bool fast = need <= nrec && yr_range_ok(g.in_h, (int)S.pitch, need);
     const uint64_t sbu = reinterpret_cast<uint64_t>(S.base);
     Hp2Block B;
-    // records: to the image end, or (IPP_HP_YRANGE) only to one byte past the
-    // window's last pixel, so that a row above or below the window is out of
-    // range (row y ≥ in_h starts at y·pitch ≥ need, as pitch ≥ in_w·CN)
-    const int nrecs = IPP_HP_YRANGE ? min(nrec, need) : nrec;
-    B.rsv = u32x4_t{(uint32_t)sbu, (uint32_t)(sbu >> 32) & 0xFFFFu, (uint32_t)nrecs, 0x00020000u};
+    // records: to the image end, or (fast) only to one byte past the window's
+    // last pixel, so that a row above or below the window is out of range
+    B.rsv = u32x4_t{(uint32_t)sbu, (uint32_t)(sbu >> 32) & 0xFFFFu, (uint32_t)(fast ? min(nrec, need) : nrec),
+                    0x00020000u};
     B.lim = S.lim;
     B.rowx = (uint32_t)S.b2 + (uint32_t)y * (uint32_t)S.b1;
     B.rowy = (uint32_t)S.b5 + (uint32_t)y * (uint32_t)S.b4;
@@ -978,10 +834,10 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
     // Fill value (raw 0): uniform over the block except for zone bits.
     const uint32_t fill = __builtin_amdgcn_readfirstlane(hsv2_px<NR, ZONES>(L.T, 0u, ~0u));  // (in an SGPR)
     const int nrows = min(HR, h.lines - row0);
-    if (CN == 3 && clamp)
-        hpass2_body<NR, ZONES, CN, true>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
-    else
+    if (fast)
         hpass2_body<NR, ZONES, CN, false>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+    else
+        hpass2_body<NR, ZONES, CN, true>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
 }
 
 // 4 waves per SIMD (≤ 128 VGPRs); the zone forms get 3 (their per-lane zone
@@ -990,89 +846,69 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
 template <int NR, bool ZONES, int CN>
 __global__ void __launch_bounds__(64 * HP_NW) __attribute__((amdgpu_waves_per_eu(ZONES ? 3 : 4)))
 k_pipe_hpass2(const uint8_t* __restrict__ src, uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
-              const ipp_pipe_desc* __restrict__ descs, int n, int tiles_y, ipp_hsv_params hp,
+              const ipp_pipe_desc* __restrict__ descs, int n, FastDiv tiles_y, FastDiv per_grp, ipp_hsv_params hp,
               const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst) {
     __shared__ Hpass2Lds<NR> L;
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    // tiles_y = H-pass blocks per item.  Each group of kCopyGroup items owns
-    // its items' H-pass blocks followed by kCopySlabs background-copy blocks,
-    // so the copies run beside the H pass on every XCD.
-    const int per_grp = kCopyGroup * tiles_y + kCopySlabs;
-    const int grp = b / per_grp;
-    const int t = b - grp * per_grp;
-    if (t >= kCopyGroup * tiles_y) {
-#if !(defined(IPP_DIAG) && defined(IPP_DIAG_NOCOPY))  // diagnostic (wrong output): no background copy
-        bg_copy_group<64 * HP_NW>(descs, n, grp * kCopyGroup, t - kCopyGroup * tiles_y, bg, dst);
-#endif
+    // tiles_y = H-pass blocks per item (one per band).  Each group of
+    // kCopyGroup items owns its items' H-pass blocks followed by kCopySlabs
+    // background-copy blocks (per_grp = kCopyGroup·tiles_y + kCopySlabs), so
+    // the copies run beside the H pass on every XCD.
+    const int ty = (int)tiles_y.d;
+    const int grp = (int)fdiv(b, per_grp);
+    const int t = (int)(b - (uint32_t)grp * per_grp.d);
+    if (t >= kCopyGroup * ty) {
+        bg_copy_group<64 * HP_NW>(descs, n, grp * kCopyGroup, t - kCopyGroup * ty, bg, dst);
         return;
     }
-#if defined(IPP_DIAG) && defined(IPP_DIAG_COPY_ONLY)
-    return;  // diagnostic (wrong output): the copy blocks alone
-#endif
-    const int j = t / tiles_y;
+    const int j = (int)fdiv((uint32_t)t, tiles_y);
     const int im = grp * kCopyGroup + j;
     if (im >= n) return;
-    hpass_block<NR, ZONES, CN>(L, src, tmp, coefs, descs, im, t - j * tiles_y, hp);
+    hpass_block<NR, ZONES, CN>(L, src, tmp, coefs, descs, im, t - j * ty, hp);
 }
 
 // V pass on MFMA (tap tiles aligned with 16-row background bands: the plan's
-// phase = p.y mod 16) → unpremultiply → blend onto the background, fused with
-// the background copy.  Block = 16 composite rows of one item.  A = taps of
-// the band's 16 overlay rows (lane l: row l&15, T rows 16(l>>4)..+15 of the K
-// step), B = 64 T rows × 16 overlay columns of one channel (four 16-B T groups
-// per lane give all four channels), D lane l = column l&15, rows 4(l>>4)..+3.
+// phase = p.y mod 16) → unpremultiply → blend onto the background.  Block =
+// 16 composite rows of one item.  A = taps of the band's 16 overlay rows (lane
+// l: row l&15, T rows 16(l>>4)..+15 of the K step), B = 64 T rows × 16
+// overlay columns of one channel (four 16-B T groups per lane give all four
+// channels), D lane l = column l&15, rows 4(l>>4)..+3.
+//
+// Horner accumulation over the tap byte planes (round 6): one accumulator per
+// channel instead of one per (channel, plane) — plane 2's products summed over
+// every K step, shifted left by 8, plane 1's added, shifted again with the row
+// bias added (v_lshl_add), then plane 0's: ((S2 << 8) + S1) << 8 + bias + S0
+// equals planes3(bias + S0, S1, S2) in int32 wrap-around arithmetic.  It
+// frees 32 VGPRs of the 48 the accumulators took.
 constexpr int VBR = 16;
 // V pass: column tiles with nK ≤ IPP_VB_DB double-buffer their T groups (the
-// wave's next tile's loads fly during this tile's MFMAs).  At 3 waves/SIMD
-// with every nK ≤ 4 hoisted, DB 2 took 1.414-1.418 -> 1.399 ms (nK 3 spills
-// 65 VGPRs); at 4 waves (below) only nK 1 is hoisted and double-buffered.
-// Unpremultiply by a per-block LDS table of magic divisors (exact,
-// unpremultiply_magic) instead of a reciprocal and two fix-ups per channel:
-// 1.340 -> 1.319 ms (round 5, alternating runs on one box,
-// profiles/r05/vpass/ab_unpremul_magic_r05al.txt).
-#ifndef IPP_VB_MAGIC
-#define IPP_VB_MAGIC 1
-#endif
+// wave's next tile's loads fly during this tile's MFMAs).
 #ifndef IPP_VB_DB
 #define IPP_VB_DB 2
 #endif
 // V pass: the band's taps loaded once for all its column tiles (nK ≤
 // IPP_VB_HOIST_MAX; larger nK load each K step's taps per column tile).  Of
-// the bench's V tiles 7 % have nK 1, 74 % nK 2, 19 % nK 3.  Hoisting only nK
-// ≤ 2 or only nK 1 lets the pass run at 4 waves/SIMD (128 / 106 VGPRs):
-// 1.402 / 1.547 ms against 1.400 at 3 waves with nK ≤ 4 hoisted (round 5,
-// one box, parity green for all three; profiles/r05/vpass/).
+// the bench's V tiles 7 % have nK 1, 74 % nK 2, 19 % nK 3.
 #ifndef IPP_VB_HOIST_MAX
-#define IPP_VB_HOIST_MAX 4
+#define IPP_VB_HOIST_MAX 3
 #endif
-#ifndef IPP_VB_HOIST
-#define IPP_VB_HOIST 1
-#endif
-// V pass, background loads of the composite phase (experiment switch): 0 =
-// the next step's issued right after this step's stores, 1 = one step ahead
-// and the first step's before the MFMA phase, 2 = one step ahead.  At 3
-// waves/SIMD: 1.400 / 1.416 / 1.422-1.424 ms for 1 / 2 / 0 (round 5, one box;
-// at 2 waves/SIMD 1 was 14 % slower than 2), but 1 spills 2 VGPRs at 3 waves:
-// 2 kept.
-#ifndef IPP_VB_PF
-#define IPP_VB_PF 2
-#endif
-// Diagnostic builds only (-DIPP_DIAG -DIPP_VB_X=…, wrong output): bit 0 = no
-// blend, bit 1 = no unpremultiply, bit 2 = no background copy loop.
-#if defined(IPP_DIAG) && defined(IPP_VB_X)
-constexpr int kVbX = IPP_VB_X;
-#else
-constexpr int kVbX = 0;
+// V pass occupancy target (waves per SIMD).  Round 5 (three accumulators per
+// channel): 3 fit 160 VGPRs with every nK ≤ 4 hoisted (the compiler's own
+// choice, 168 VGPRs + 52 AGPRs, gave 2 waves): 1.49-1.52 -> 1.37-1.40 ms.
+#ifndef IPP_VB_WPE
+#define IPP_VB_WPE 3
 #endif
 
 // orow (the band's unpremultiplied overlay rows in LDS) is indexed by
 // composite column - (p.x & ~15), so a 16-pixel composite group reads its 16
 // overlay pixels with four aligned ds_read_b128; the ≤ 15 columns before the
-// overlay and after it are zero (α 0: the background stays).  (A
-// quarter-planar layout that makes those reads conflict-free measured 0 on
-// the split V pass and -0.5 % on the fused launch, and spilled in one fused
-// instantiation: not kept.)
+// overlay and after it are zero (α 0: the background stays).
 __host__ __device__ constexpr int orow_stride(int ov_w_max) { return (ov_w_max + 32 + 3) & ~3; }
+// The widest overlay the V launch takes: its rows must fit 64 KB of LDS
+// (IPP_PIPE_MAX_OV_W in ipp.h; the magic-divisor table is dropped for
+// overlays too wide to hold it beside the rows).
+static_assert((size_t)VBR * orow_stride(IPP_PIPE_MAX_OV_W) * 4 <= 64 * 1024, "V-pass rows in LDS");
+static_assert((size_t)VBR * orow_stride(IPP_PIPE_MAX_OV_W + 1) * 4 > 64 * 1024, "IPP_PIPE_MAX_OV_W is the limit");
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -1110,9 +946,52 @@ __device__ __forceinline__ void blend48(uint32_t (&bg)[12], const uint32_t (&ov)
     }
 }
 
+// acc = (acc << 8) + (a0, a1, a2, a3) (Horner step; the compiler emits one
+// v_lshl_add_u32 per dword.  Plain code, not inline asm: the MFMA results it
+// reads need the wait states the compiler's hazard recognizer inserts, which
+// it does not do for an asm operand.)
+__device__ __forceinline__ void horner8(i32x4& acc, int32_t a0, int32_t a1, int32_t a2, int32_t a3) {
+    acc = (acc << 8) + i32x4{a0, a1, a2, a3};
+}
+
+// Channel c's B operand of one K step: dword c of its four T groups (a
+// register transpose the MFMA needs anyway: its source tuple must be four
+// consecutive registers).
+__device__ __forceinline__ i32x4 vb_bop(const u32x4_t (&g)[4], int c) {
+    return i32x4{(int)g[0][c], (int)g[1][c], (int)g[2][c], (int)g[3][c]};
+}
+
+// One column tile's V sums, Horner over the tap byte planes (see above):
+// plane 2's MFMAs over all NK K steps, << 8, plane 1's, << 8 with the row
+// biases, plane 0's.  bq = the channel-major B operands (vb_bop) per K step.
+template <int NK>
+__device__ __forceinline__ void vb_mfma_tile(const i32x4 (&ta)[NK][3], const i32x4 (&bq)[NK][4], const int32_t (&rb)[4],
+                                             i32x4 (&acc)[4]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = i32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int q = 2; q >= 0; --q) {
+#pragma unroll
+        for (int ks = 0; ks < NK; ++ks)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ta[ks][q], bq[ks][c], acc[c], 0, 0, 0);
+        if (q == 2) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] <<= 8;
+        } else if (q == 1) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) horner8(acc[c], rb[0], rb[1], rb[2], rb[3]);
+        }
+    }
+}
+
 // One V-pass block: band ty of item im, counted from the first 16-row band
 // the overlay touches (the rows outside those bands: ipp_pipe_hpass_bgcopy).
-template <int STORE, int DBG>
+// MAGIC: unpremultiply by the per-block LDS table of magic divisors (exact,
+// unpremultiply_magic) instead of a reciprocal and two fix-ups per channel:
+// 1.340 -> 1.319 ms (round 5, profiles/r05/vpass/ab_unpremul_magic_r05al.txt);
+// overlays too wide for the table beside their rows take the reciprocal.
+template <bool MAGIC>
 __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const uint8_t* __restrict__ tmp,
                                              const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
                                              const int32_t* __restrict__ coefs,
@@ -1128,18 +1007,15 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
     if (y0 >= p.bg_h) return;
     const int nrows = min(VBR, p.bg_h - y0);
     const int oy_lo = max(0, y0 - p.y), oy_hi = min(p.ov_h, y0 + nrows - p.y);
-    const bool any = (DBG & 2) ? false : oy_lo < oy_hi;  // block-uniform
+    const bool any = oy_lo < oy_hi;  // block-uniform
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
     const int os = orow_stride(ov_w_max), xo = p.x & 15;  // orow column of overlay column 0
-    // Phase-2 geometry, and (IPP_VB_PF) the thread's first background group
-    // loaded now so that its latency hides behind phase 1.
     const uint8_t* bgb = bg + p.bg_off + (int64_t)y0 * p.bg_pitch;
     uint8_t* dsb = dst + p.dst_off + (int64_t)y0 * p.dst_pitch;
     const bool groups = (p.bg_w & 15) == 0 && ((p.bg_pitch | p.dst_pitch) & 15) == 0 &&
-                        ((reinterpret_cast<uintptr_t>(bgb) | reinterpret_cast<uintptr_t>(dsb)) & 15u) == 0 &&
-                        !(DBG & 1) && !(kVbX & 4);
+                        ((reinterpret_cast<uintptr_t>(bgb) | reinterpret_cast<uintptr_t>(dsb)) & 15u) == 0;
     // groups per row visited: all of them, or (column split) the overlay's
     // [sx0, sx1) — the H pass's copy blocks wrote the rest of the band rows
     int sx0, sx1;
@@ -1156,10 +1032,9 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
         for (int q = 0; q < 3; ++q) v[q] = sp[q];
     };
     uint4 gcur[3];
-    if (IPP_VB_PF == 1 && groups && (int)threadIdx.x < gtotal) gload(threadIdx.x, gcur);
     if (any) {
-        uint32_t* umag = orow + VBR * os;  // IPP_VB_MAGIC: the unpremultiply divisors
-        if (IPP_VB_MAGIC) {
+        uint32_t* umag = orow + VBR * os;  // MAGIC: the unpremultiply divisors
+        if (MAGIC) {
             umag[threadIdx.x] = unpremul_magic(threadIdx.x);
             __syncthreads();
         }
@@ -1180,127 +1055,124 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
         const int ctiles = (p.ov_w + 15) >> 4;
         const int gstride = v.src_pitch >> 4;  // uint4 per T group row
         const int x_l = lane & 15;
-        // the row biases ride in the first byte plane's initial accumulators
+        // the row biases (added at the last Horner step)
         int32_t rb[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) rb[r] = tbias[16 * t + 4 * (lane >> 4) + r];
+        const u32x4_t* tbase = reinterpret_cast<const u32x4_t*>(tmp + v.src_off);
+        const int gbase = (th.x + 16 * (lane >> 4)) >> 2;
+        // T groups of K step ks of column tile ct: rows th.x + 64 ks + 16 (lane >> 4) .. + 15
+        auto tload = [&](int ct, int ks, u32x4_t (&g)[4]) {
+            const int xs = min(16 * ct + x_l, p.ov_w - 1);
+            const u32x4_t* tq = tbase + xs + (int64_t)(gbase + 16 * ks) * gstride;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) g[j] = tq[j * gstride];
+        };
+        // the tile's unpremultiplied overlay pixels into the band's LDS rows
+        // (s(c, r) = the sum of channel c, tile row r)
+        auto epilogue = [&](int ct, auto s) {
+            const int x = 16 * ct + x_l;
+            if (x < p.ov_w) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 4 * (lane >> 4) + r;  // band row = tile row
+                    const int o = y0 + row - p.y;         // overlay row
+                    if (o >= oy_lo && o < oy_hi) {
+                        const uint32_t px = clip8x4_mfma(s(0, r), s(1, r), s(2, r), s(3, r));
+                        orow[row * os + xo + x] = MAGIC ? unpremultiply_magic(px, umag) : unpremultiply(px);
+                    }
+                }
+            }
+        };
         // The band's taps (the A operand) are the same for every column tile:
-        // with nK ≤ 4 they are loaded once, before the column tiles, and every
-        // tile's T groups for all its K steps are issued before its MFMAs.
+        // with nK ≤ IPP_VB_HOIST_MAX they are loaded once, before the column
+        // tiles, and every tile's T groups for all its K steps are issued
+        // before its MFMAs.
         auto tiles = [&](auto nkc) {
             constexpr int NK = decltype(nkc)::value;
-            i32x4 ta[NK > 0 ? NK : 1][3];
-            if (NK > 0) {
+            if constexpr (NK > 0) {
+                i32x4 ta[NK][3];
 #pragma unroll
                 for (int ks = 0; ks < NK; ++ks)
 #pragma unroll
                     for (int q = 0; q < 3; ++q)
                         ta[ks][q] = __builtin_bit_cast(i32x4, tblk[th.z + (ks * 3 + q) * 64 + lane]);
-            }
-            const uint4* tbase = reinterpret_cast<const uint4*>(tmp + v.src_off);
-            const int gbase = (th.x + 16 * (lane >> 4)) >> 2;
-            // T groups of K step ks of column tile ct: rows th.x + 64 ks + 16 (lane >> 4) .. + 15
-            auto tload = [&](int ct, int ks, uint4 (&g)[4]) {
-                const int xs = min(16 * ct + x_l, p.ov_w - 1);
-                const uint4* tq = tbase + xs + (int64_t)(gbase + 16 * ks) * gstride;
+                // the loaded T groups of a tile, turned channel-major
+                auto transpose = [&](const u32x4_t (&g)[NK][4], i32x4 (&bq)[NK][4]) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) g[j] = tq[j * gstride];
-            };
-#define IPP_VB_MFMA(a, g)                                                                    \
-    {                                                                                        \
-        const i32x4 bq[4] = {i32x4{(int)(g)[0].x, (int)(g)[1].x, (int)(g)[2].x, (int)(g)[3].x}, \
-                             i32x4{(int)(g)[0].y, (int)(g)[1].y, (int)(g)[2].y, (int)(g)[3].y}, \
-                             i32x4{(int)(g)[0].z, (int)(g)[1].z, (int)(g)[2].z, (int)(g)[3].z}, \
-                             i32x4{(int)(g)[0].w, (int)(g)[1].w, (int)(g)[2].w, (int)(g)[3].w}}; \
-        _Pragma("unroll") for (int c = 0; c < 4; ++c)                                        \
-            _Pragma("unroll") for (int q = 0; q < 3; ++q)                                    \
-                acc[c][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8((a)[q], bq[c], acc[c][q], 0, 0, 0); \
-    }
-#define IPP_VB_ACC_INIT                                          \
-    _Pragma("unroll") for (int c = 0; c < 4; ++c) {              \
-        acc[c][0] = i32x4{rb[0], rb[1], rb[2], rb[3]};           \
-        acc[c][1] = i32x4{0, 0, 0, 0};                           \
-        acc[c][2] = i32x4{0, 0, 0, 0};                           \
-    }
-// the tile's unpremultiplied overlay pixels into the band's LDS rows
-#define IPP_VB_EPILOGUE(ct)                                                                     \
-    {                                                                                           \
-        const int x = 16 * (ct) + x_l;                                                          \
-        if (x < p.ov_w) {                                                                       \
-            _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                     \
-                const int row = 4 * (lane >> 4) + r; /* band row = tile row */                  \
-                const int o = y0 + row - p.y;        /* overlay row */                          \
-                if (o >= oy_lo && o < oy_hi) {                                                  \
-                    int32_t ss[4];                                                              \
-                    _Pragma("unroll") for (int c = 0; c < 4; ++c)                               \
-                        ss[c] = planes3(acc[c][0][r], acc[c][1][r], acc[c][2][r]);               \
-                    const uint32_t px = clip8x4(ss[0], ss[1], ss[2], ss[3]);                    \
-                    orow[row * os + xo + x] = (kVbX & 2) ? px : IPP_VB_MAGIC ? unpremultiply_magic(px, umag) : unpremultiply(px); \
-                }                                                                               \
-            }                                                                                   \
-        }                                                                                       \
-    }
-            if constexpr (NK > 0 && NK <= IPP_VB_DB) {
-                // double-buffered T groups: the wave's next column tile's
-                // loads are in flight during this tile's MFMAs and epilogue
-                uint4 gc[NK][4], gn[NK][4];
-                int ct = wave;
-                if (ct < ctiles) {
+                    for (int ks = 0; ks < NK; ++ks)
 #pragma unroll
-                    for (int ks = 0; ks < NK; ++ks) tload(ct, ks, gc[ks]);
-                }
-                for (; ct < ctiles; ct += 4) {
-                    const bool more = ct + 4 < ctiles;
-                    if (more) {
+                        for (int c = 0; c < 4; ++c) bq[ks][c] = vb_bop(g[ks], c);
+                };
+                if constexpr (NK <= IPP_VB_DB) {
+                    // double-buffered T groups: the wave's next column tile's
+                    // loads are in flight during this tile's MFMAs and
+                    // epilogue; the buffer carried to the next tile is the
+                    // channel-major operands, so raw and transposed groups
+                    // are never live together
+                    i32x4 bc[NK][4];
+                    u32x4_t gn[NK][4];
+                    int ct = wave;
+                    if (ct < ctiles) {
 #pragma unroll
-                        for (int ks = 0; ks < NK; ++ks) tload(ct + 4, ks, gn[ks]);
+                        for (int ks = 0; ks < NK; ++ks) tload(ct, ks, gn[ks]);
+                        transpose(gn, bc);
                     }
-                    i32x4 acc[4][3];
-                    IPP_VB_ACC_INIT
+                    for (; ct < ctiles; ct += 4) {
+                        const bool more = ct + 4 < ctiles;
+                        if (more) {
 #pragma unroll
-                    for (int ks = 0; ks < NK; ++ks) IPP_VB_MFMA(ta[ks], gc[ks])
-                    IPP_VB_EPILOGUE(ct)
-                    if (more) {
+                            for (int ks = 0; ks < NK; ++ks) tload(ct + 4, ks, gn[ks]);
+                        }
+                        i32x4 acc[4];
+                        vb_mfma_tile<NK>(ta, bc, rb, acc);
+                        epilogue(ct, [&](int c, int r) { return acc[c][r]; });
+                        if (more) transpose(gn, bc);
+                    }
+                } else {
+                    for (int ct = wave; ct < ctiles; ct += 4) {
+                        u32x4_t g[NK][4];
 #pragma unroll
-                        for (int ks = 0; ks < NK; ++ks)
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) gc[ks][j] = gn[ks][j];
+                        for (int ks = 0; ks < NK; ++ks) tload(ct, ks, g[ks]);
+                        i32x4 bq[NK][4];
+                        transpose(g, bq);
+                        i32x4 acc[4];
+                        vb_mfma_tile<NK>(ta, bq, rb, acc);
+                        epilogue(ct, [&](int c, int r) { return acc[c][r]; });
                     }
                 }
             } else {
-            for (int ct = wave; ct < ctiles; ct += 4) {
-                i32x4 acc[4][3];
-                IPP_VB_ACC_INIT
-                if (NK > 0) {
-                    // (loading the next column tile's T groups here, before
-                    // this tile's MFMAs, measured +9 % at 2 waves/SIMD; see
-                    // IPP_VB_DB for the double-buffered form)
-                    uint4 g[NK > 0 ? NK : 1][4];
+                // nK beyond the hoisted forms: each K step's taps and T groups
+                // loaded in turn, one accumulator per (channel, plane)
+                for (int ct = wave; ct < ctiles; ct += 4) {
+                    i32x4 acc[4][3];
 #pragma unroll
-                    for (int ks = 0; ks < NK; ++ks) tload(ct, ks, g[ks]);
-#pragma unroll
-                    for (int ks = 0; ks < NK; ++ks) IPP_VB_MFMA(ta[ks], g[ks])
-                } else {
+                    for (int c = 0; c < 4; ++c) {
+                        acc[c][0] = i32x4{rb[0], rb[1], rb[2], rb[3]};
+                        acc[c][1] = i32x4{0, 0, 0, 0};
+                        acc[c][2] = i32x4{0, 0, 0, 0};
+                    }
 #pragma unroll 1
                     for (int ks = 0; ks < th.y; ++ks) {
                         i32x4 a[3];
 #pragma unroll
-                        for (int q = 0; q < 3; ++q)
-                            a[q] = __builtin_bit_cast(i32x4, tblk[th.z + (ks * 3 + q) * 64 + lane]);
-                        uint4 g[4];
+                        for (int q = 0; q < 3; ++q) a[q] = __builtin_bit_cast(i32x4, tblk[th.z + (ks * 3 + q) * 64 + lane]);
+                        u32x4_t g[4];
                         tload(ct, ks, g);
-                        IPP_VB_MFMA(a, g)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const i32x4 bq = vb_bop(g, c);
+#pragma unroll
+                            for (int q = 0; q < 3; ++q)
+                                acc[c][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[q], bq, acc[c][q], 0, 0, 0);
+                        }
                     }
+                    epilogue(ct, [&](int c, int r) { return planes3(acc[c][0][r], acc[c][1][r], acc[c][2][r]); });
                 }
-                IPP_VB_EPILOGUE(ct)
             }
-            }
-#undef IPP_VB_ACC_INIT
-#undef IPP_VB_EPILOGUE
-#undef IPP_VB_MFMA
         };
         // (a tile with more K steps than IPP_VB_HOIST_MAX takes the generic loop)
-        switch (IPP_VB_HOIST && th.y <= IPP_VB_HOIST_MAX ? th.y : 0) {
+        switch (th.y <= IPP_VB_HOIST_MAX ? th.y : 0) {
             case 1: tiles(std::integral_constant<int, 1>{}); break;
 #if IPP_VB_HOIST_MAX >= 2
             case 2: tiles(std::integral_constant<int, 2>{}); break;
@@ -1320,14 +1192,13 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
     const int row_bytes = 3 * p.bg_w;
     if (groups) {
         // 16-pixel groups: 48 bytes per thread and step (three 16-B loads in
-        // flight; with IPP_VB_PF the next step's loads are issued before this
-        // step's blend and stores), the overlay pixels from orow, blended in
-        // 16-bit lanes.
+        // flight; the next step's loads are issued before this step's blend
+        // and stores), the overlay pixels from orow, blended in 16-bit lanes.
         const int gx0 = p.x >> 4, gx1 = (p.x + p.ov_w + 15) >> 4;  // groups the overlay touches
-        if (IPP_VB_PF != 1 && (int)threadIdx.x < gtotal) gload(threadIdx.x, gcur);
+        if ((int)threadIdx.x < gtotal) gload(threadIdx.x, gcur);
         for (int idx = threadIdx.x; idx < gtotal; idx += 256) {
             uint4 gnxt[3];
-            if (IPP_VB_PF >= 1 && idx + 256 < gtotal) gload(idx + 256, gnxt);
+            if (idx + 256 < gtotal) gload(idx + 256, gnxt);
             const int rr = pow2 ? idx >> lg : idx / G;
             const int gi = gc0 + idx - rr * G;
             uint32_t w[12];
@@ -1339,7 +1210,7 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
                 w[4 * q + 3] = gcur[q].w;
             }
             const int o = y0 + rr - p.y;
-            if (!(kVbX & 1) && any && o >= oy_lo && o < oy_hi && gi >= gx0 && gi < gx1) {
+            if (any && o >= oy_lo && o < oy_hi && gi >= gx0 && gi < gx1) {
                 const uint4* orw = reinterpret_cast<const uint4*>(orow + rr * os + 16 * (gi - gx0));
                 uint32_t ov[16];
 #pragma unroll
@@ -1352,22 +1223,20 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
                 }
                 blend48(w, ov);
             }
+            // plain stores (nt 1.356, sc1 1.581 against 1.335 ms; round 5,
+            // profiles/r05/vpass/ab_vstore_policy_r05af.txt)
             uint8_t* dp = dsb + (int64_t)rr * p.dst_pitch + 48 * gi;
 #pragma unroll
-            for (int q = 0; q < 3; ++q) store16<STORE>(dp + 16 * q, 16, true, w + 4 * q);
-            if (IPP_VB_PF >= 1) {
+            for (int q = 0; q < 3; ++q) store16<0>(dp + 16 * q, 16, true, w + 4 * q);
 #pragma unroll
-                for (int q = 0; q < 3; ++q) gcur[q] = gnxt[q];
-            } else if (idx + 256 < gtotal) {
-                gload(idx + 256, gcur);
-            }
+            for (int q = 0; q < 3; ++q) gcur[q] = gnxt[q];
         }
         return;
     }
     // General layout: 16-B chunks, byte-wise blend.  Four chunks per thread are
     // loaded before any is stored, so each wave keeps four reads in flight.
     const int chunks = (row_bytes + 15) >> 4;
-    const int total = (kVbX & 4) ? 0 : nrows * chunks;
+    const int total = nrows * chunks;
     for (int base = threadIdx.x; base < total; base += 4 * 256) {
         uint32_t w[4][4];
         int rr[4], c0[4], nb[4];
@@ -1379,70 +1248,48 @@ __device__ __forceinline__ void vblend_block(uint32_t* __restrict__ orow, const 
             nb[u] = idx < total ? min(16, row_bytes - c0[u]) : 0;
             if (nb[u] > 0) {
                 const uint8_t* bp = bg + p.bg_off + (int64_t)(y0 + rr[u]) * p.bg_pitch + c0[u];
-                if (DBG & 1) {
-                    w[u][0] = w[u][1] = w[u][2] = w[u][3] = (uint32_t)c0[u];
-                } else {
-                    load16(bp, nb[u], nb[u] == 16 && (reinterpret_cast<uintptr_t>(bp) & 15u) == 0, w[u]);
-                }
+                load16(bp, nb[u], nb[u] == 16 && (reinterpret_cast<uintptr_t>(bp) & 15u) == 0, w[u]);
             }
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (nb[u] <= 0) continue;
             const int o = y0 + rr[u] - p.y;
-            if (!(kVbX & 1) && any && o >= oy_lo && o < oy_hi && c0[u] + nb[u] > 3 * p.x && c0[u] < 3 * (p.x + p.ov_w)) {
+            if (any && o >= oy_lo && o < oy_hi && c0[u] + nb[u] > 3 * p.x && c0[u] < 3 * (p.x + p.ov_w)) {
                 const uint32_t* orw = orow + rr[u] * os + xo;
                 blend16(w[u], c0[u], nb[u], p.x, p.ov_w, [&](int ox) { return orw[ox]; });
             }
             uint8_t* dp = dst + p.dst_off + (int64_t)(y0 + rr[u]) * p.dst_pitch + c0[u];
-            store16<STORE>(dp, nb[u], nb[u] == 16 && (reinterpret_cast<uintptr_t>(dp) & 15u) == 0, w[u]);
+            store16<0>(dp, nb[u], nb[u] == 16 && (reinterpret_cast<uintptr_t>(dp) & 15u) == 0, w[u]);
         }
     }
 }
 
-// V pass occupancy target (waves per SIMD).  With every nK ≤ 4 hoisted, 3
-// fit 160 VGPRs (the compiler's own choice, 168 VGPRs + 52 AGPRs, gave 2
-// waves): 1.49-1.52 -> 1.37-1.40 ms (round 5; round 3 measured no difference
-// with the full-width band rows still in the pass), and 4 spilled 54 VGPRs;
-// with only nK 1 hoisted (IPP_VB_HOIST_MAX) 4 fit 128 VGPRs (5: 50 spills).
-#ifndef IPP_VB_WPE
-#define IPP_VB_WPE 3
-#endif
-// Composite store policy (store16): plain / sc1 / nt 1.335 / 1.581 / 1.356 ms
-// (round 5, alternating runs on one box, profiles/r05/vpass/ab_vstore_policy_r05af.txt).
-#ifndef IPP_VB_STPOL
-#define IPP_VB_STPOL 0
-#endif
 #if IPP_VB_WPE > 0
 #define IPP_VB_ATTR __attribute__((amdgpu_waves_per_eu(IPP_VB_WPE)))
 #else
 #define IPP_VB_ATTR
 #endif
-template <int STORE, int DBG = 0>
+template <bool MAGIC>
 __global__ void __launch_bounds__(256) IPP_VB_ATTR
 k_pipe_vblend_mfma(const uint8_t* __restrict__ tmp, const uint8_t* __restrict__ bg, uint8_t* __restrict__ dst,
-                   const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, int tiles_y,
+                   const int32_t* __restrict__ coefs, const ipp_pipe_desc* __restrict__ descs, FastDiv tiles_y,
                    int ov_w_max) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t orow[];  // [VBR][orow_stride(ov_w_max)]
+    extern __shared__ __attribute__((aligned(16))) uint32_t orow[];  // [VBR][orow_stride(ov_w_max)] (+ 256 divisors)
     const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int im = b / tiles_y;
-    const int ty = b - im * tiles_y;
-    vblend_block<STORE, DBG>(orow, tmp, bg, dst, coefs, descs, im, ty, ov_w_max);
+    const int im = (int)fdiv(b, tiles_y);
+    const int ty = (int)(b - (uint32_t)im * tiles_y.d);
+    vblend_block<MAGIC>(orow, tmp, bg, dst, coefs, descs, im, ty, ov_w_max);
 }
 
 template <int NR, bool ZONES, int CN>
 void launch_hpass(int n, int ty, hipStream_t s, const uint8_t* src, uint8_t* tmp, const int32_t* coefs,
                   const ipp_pipe_desc* descs, const ipp_hsv_params& hp, const uint8_t* bg, uint8_t* dst) {
-#ifdef IPP_DIAG
-    // diagnostic: unused dynamic LDS per block, to cap the blocks per CU
-    static const size_t pad = (size_t)diag_env("IPP_HP_PAD", 0);
-#else
-    constexpr size_t pad = 0;
-#endif
     // H pass + the background outside the overlays, per group of kCopyGroup items
     const int64_t groups = (n + kCopyGroup - 1) / kCopyGroup;
-    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), dim3((uint32_t)(groups * (kCopyGroup * ty + kCopySlabs))),
-                       dim3(64 * HP_NW), pad, s, src, tmp, coefs, descs, n, ty, hp, bg, dst);
+    const uint32_t per_grp = (uint32_t)(kCopyGroup * ty + kCopySlabs);
+    hipLaunchKernelGGL((k_pipe_hpass2<NR, ZONES, CN>), dim3((uint32_t)(groups * per_grp)), dim3(64 * HP_NW), 0, s,
+                       src, tmp, coefs, descs, n, fast_div((uint32_t)ty), fast_div(per_grp), hp, bg, dst);
 }
 
 template <int NR>
@@ -1469,10 +1316,7 @@ extern "C" int ipp_pipe_hpass_bgcopy(const uint8_t* src, uint8_t* tmp, const int
         return IPP_E_ARG;
     if (src_cn != 3 && src_cn != 4) return IPP_E_ARG;
     if (tap_format != IPP_TAPS_MFMA) return IPP_E_ARG;
-    int ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
-#ifdef IPP_EMPTY_X2
-    ty *= 2;  // experiment: as many empty blocks again (their cost)
-#endif
+    const int ty = (max_rows + HR - 1) / HR;  // one block per 16-row band
     if ((int64_t)(kCopyGroup * ty + kCopySlabs) * ((n_images + kCopyGroup - 1) / kCopyGroup) >= INT32_MAX)
         return IPP_E_ARG;
     hipStream_t s = (hipStream_t)stream;
@@ -1525,30 +1369,24 @@ extern "C" int ipp_pipe_vblend_bands(const uint8_t* tmp, const uint8_t* bg, uint
                                      int32_t max_ov_w, int32_t max_ov_h, int32_t tap_format, void* stream) {
     if (n_images == 0) return IPP_OK;
     if (!tmp || !bg || !dst || !coefs || !descs || n_images < 0 || bg_w <= 0 || bg_h <= 0) return IPP_E_ARG;
-    if (tap_format != IPP_TAPS_MFMA || max_ov_w <= 0 || max_ov_w > bg_w || max_ov_h <= 0 || max_ov_h > bg_h)
+    if (tap_format != IPP_TAPS_MFMA || max_ov_w <= 0 || max_ov_w > bg_w || max_ov_h <= 0 || max_ov_h > bg_h ||
+        max_ov_w > IPP_PIPE_MAX_OV_W)
         return IPP_E_ARG;
-    const size_t sm = ((size_t)VBR * orow_stride(max_ov_w) + 256) * sizeof(uint32_t);  // + the magic divisors
+    const size_t rows = (size_t)VBR * orow_stride(max_ov_w) * sizeof(uint32_t);
+    const size_t magic = 256 * sizeof(uint32_t);  // the unpremultiply divisors, when they fit beside the rows
+    const bool use_magic = rows + magic <= 64 * 1024;
     // an overlay of height H at any y spans at most ceil((15 + H) / 16) bands
-    int tyb = std::min((max_ov_h + 15 + VBR - 1) / VBR, (bg_h + VBR - 1) / VBR);
-#ifdef IPP_EMPTY_X2
-    tyb *= 2;  // experiment: as many empty blocks again (their cost)
-#endif
+    const int tyb = std::min((max_ov_h + 15 + VBR - 1) / VBR, (bg_h + VBR - 1) / VBR);
     const int64_t nb = (int64_t)tyb * n_images;
-    if (nb >= INT32_MAX || sm > 64 * 1024) return IPP_E_ARG;
+    if (nb >= INT32_MAX) return IPP_E_ARG;
     hipStream_t st = (hipStream_t)stream;
-#ifdef IPP_DIAG
-    // experiment kernels (WRONG output): 9 no background reads, 10 no V pass, 11 stores only
-    static const int pol = diag_env("IPP_VB_STORE", 2);
-    switch (pol) {
-        case 9: hipLaunchKernelGGL((k_pipe_vblend_mfma<IPP_VB_STPOL, 1>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-        case 10: hipLaunchKernelGGL((k_pipe_vblend_mfma<IPP_VB_STPOL, 2>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-        case 11: hipLaunchKernelGGL((k_pipe_vblend_mfma<IPP_VB_STPOL, 3>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-        default: hipLaunchKernelGGL((k_pipe_vblend_mfma<IPP_VB_STPOL, 0>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst, coefs, descs, tyb, max_ov_w); break;
-    }
-#else
-    hipLaunchKernelGGL((k_pipe_vblend_mfma<IPP_VB_STPOL, 0>), dim3((uint32_t)nb), dim3(256), sm, st, tmp, bg, dst,
-                       coefs, descs, tyb, max_ov_w);
-#endif
+    const FastDiv ftyb = fast_div((uint32_t)tyb);
+    if (use_magic)
+        hipLaunchKernelGGL(k_pipe_vblend_mfma<true>, dim3((uint32_t)nb), dim3(256), rows + magic, st, tmp, bg, dst,
+                           coefs, descs, ftyb, max_ov_w);
+    else
+        hipLaunchKernelGGL(k_pipe_vblend_mfma<false>, dim3((uint32_t)nb), dim3(256), rows, st, tmp, bg, dst, coefs,
+                           descs, ftyb, max_ov_w);
     IPP_CHECK_LAUNCH();
     return IPP_OK;
 }

@@ -91,9 +91,6 @@ __device__ __forceinline__ void gather4_issue_sq8(const Sampler& S, uint32_t xx,
             G.sh[k] = (off - offc) << 3;
             off = offc;
         }
-#ifdef IPP_DBG_ALIGNED_GATHER
-        off &= ~3u;  // diagnostics (wrong output): aligned dword gathers
-#endif
         G.raw[k] = *reinterpret_cast<const ipp_u32_unaligned*>(S.base + off);
         G.valid |= (ok ? 1u : 0u) << k;
     }

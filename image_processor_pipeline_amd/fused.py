@@ -270,6 +270,11 @@ def plan_pipe(src_hw: Tuple[int, int], n: int, bg_hw: Tuple[int, int], n_bg: int
         raise exc(f"item {int(tot[N.PT['err_item']])}: {msg}")
     N.check(rc, "ipp_plan_pipe_batch")
     T = {k: int(tot[v]) for k, v in N.PT.items()}
+    if T["max_ov_w"] > N.IPP_PIPE_MAX_OV_W:
+        # refused here, before either launch: the V launch holds an overlay's
+        # 16 rows in 64 KB of LDS (ipp.h IPP_PIPE_MAX_OV_W)
+        raise ValueError(f"overlay width {T['max_ov_w']} px exceeds the fused pipe's limit of "
+                         f"{N.IPP_PIPE_MAX_OV_W} px (ipp_pipe_vblend_bands); use the file-mode plugins")
     hsv = G.hsv_params(cfg.hsv_ranges, cfg.zones, cfg.use_gimp_scale, bgr=False)
     return PipePlan(descs, axes, T["coef_words"], hsv, items, pool, T["tmp_bytes"], T["max_out_w"], T["max_rows"],
                     bw, bh, T["algo_h"], T["algo_v"], N.IPP_TAPS_MFMA, T["max_ov_w"], T["max_ov_h"],

@@ -114,11 +114,15 @@ class VideoChain:
         return res
 
 
-def synthetic_frames(n: int, h: int, w: int, seed: int, device, start: int = 0) -> torch.Tensor:
+def synthetic_frames(n: int, h: int, w: int, seed: int, device, start: int = 0, noise: int = 0) -> torch.Tensor:
     """Structured BGR frames: dark background (inside
     the first reference exclusion range, v <= 150), one large elliptic blob of
     a kept colour (~20 % of the area) and salt specks of random colour at
-    0.5 % density.  Frame i is drawn from its own generator (seed, start + i)."""
+    0.5 % density.  Frame i is drawn from its own generator (seed, start + i).
+    ``noise`` > 0 adds uniform ±noise LSB per channel to the background and
+    the blob (camera-like content: no 64-pixel run of one colour, so the CCL
+    mask pass's uniform-slot shortcut never applies); the classes stay the
+    same for noise ≤ 8."""
     dev = torch.device(device)
     out = torch.empty((n, h, w, 3), dtype=torch.uint8, device=dev)
     yy = torch.arange(h, device=dev, dtype=torch.float32)[:, None]
@@ -134,6 +138,9 @@ def synthetic_frames(n: int, h: int, w: int, seed: int, device, start: int = 0) 
         blob = ((xx - cx) / ax) ** 2 + ((yy - cy) / ay) ** 2 <= 1.0
         colour = torch.tensor([220, 120 + int(40 * u[4]), 40], dtype=torch.uint8, device=dev)  # blue-ish, kept
         frame[blob] = colour
+        if noise > 0:
+            d = torch.randint(-noise, noise + 1, (h, w, 3), generator=g, device=dev, dtype=torch.int16)
+            frame.copy_((frame.to(torch.int16) + d).clamp_(0, 255).to(torch.uint8))
         speck = torch.rand((h, w), generator=g, device=dev) < 0.005
         k = int(speck.sum())
         frame[speck] = torch.randint(0, 256, (k, 3), generator=g, device=dev, dtype=torch.uint8)

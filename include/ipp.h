@@ -235,7 +235,9 @@ typedef struct ipp_pipe_desc {
  * src_cn: channels of every source in the batch (3 or 4); hsv: HOST pointer;
  * tap_format: IPP_TAPS_MFMA (V axes planned with transposed = 2 + (p.y mod
  * 16), i.e. tap tiles aligned with 16-row background bands); max_ov_w /
- * max_ov_h bound the overlay sizes.
+ * max_ov_h bound the overlay sizes; ipp_pipe_vblend_bands takes overlays up
+ * to IPP_PIPE_MAX_OV_W pixels wide (their 16 rows live in 64 KB of LDS;
+ * fused.plan_pipe rejects wider ones before either launch runs).
  * Ring limit: the H pass keeps each 16-output tile's input window in a
  * 512-column LDS ring, so every H tile must satisfy 64·nK ≤ 512 (nK = its K
  * steps; ipp_plan_mfma_nk_bound(in, out, ksize) ≤ 8, i.e. LANCZOS downscales
@@ -423,6 +425,8 @@ typedef struct ipp_tap_axis {
 /* Items per background-copy group of ipp_pipe_hpass_bgcopy (one shared load
  * per background vector and run of same-background items in the group). */
 #define IPP_PIPE_COPY_GROUP 8
+/* Widest overlay (pixels) of the pipe's V launch (ipp_pipe_vblend_bands). */
+#define IPP_PIPE_MAX_OV_W 992
 
 /* items[stop - start]: outputs (inputs too when cfg->given); descs[n] (in
  * processing order), axes[2n]; totals[IPP_PLAN_TOTALS]. */

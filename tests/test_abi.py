@@ -101,5 +101,6 @@ def test_header_constants_match_the_python_mirror():
     consts = dict(re.findall(r"#define (IPP_[A-Z0-9_]+) (-?\d+)", src))
     assert int(consts["IPP_PLAN_TOTALS"]) == N.IPP_PLAN_TOTALS
     assert int(consts["IPP_PIPE_COPY_GROUP"]) == N.IPP_PIPE_COPY_GROUP
+    assert int(consts["IPP_PIPE_MAX_OV_W"]) == N.IPP_PIPE_MAX_OV_W
     for name, slot in N.PT.items():
         assert int(consts["IPP_PT_" + name.upper()]) == slot, name

@@ -219,6 +219,21 @@ def test_pipe_small_vs_oracle(D):
         assert np.array_equal(got[i], exp), i
 
 
+def test_pipe_full_width_crop_vs_oracle(D):
+    """A crop that keeps the source's full width but not its last rows
+    (margins top 3, bottom 5, left/right 0) on a dense source: pitch = 3·in_w,
+    so the gather of pixel (0, in_h) would start inside the window's buffer
+    records — these blocks must keep the row test (ipp_pipe.hip yr_range_ok;
+    round-5 advisor finding).  Random source bytes: a real pixel sampled
+    below the window in place of black would break parity."""
+    from image_processor_pipeline_amd import fused
+    cfg = fused.PipeConfig(margins=(3, 5, 0, 0))
+    src, bgs, plan, got = _run_pipe(12, 150, 170, 3, 128, 160, cfg, seed=31)
+    for i in range(len(got)):
+        exp = opipe.pipe_item(src[i], bgs, plan.params[i], cfg)
+        assert np.array_equal(got[i], exp), i
+
+
 def test_pipe_structured_content_vs_oracle(D):
     """Content that exercises the HSV ranges (dark/yellow/grey regions)."""
     from image_processor_pipeline_amd import fused
@@ -588,6 +603,23 @@ def test_video_chain_4k_vs_oracle(D):
     chain.mask(frames)
     torch.cuda.synchronize()
     assert np.array_equal(chain.bgra[0].cpu().numpy(), ops.color_mask_bgra(host[0], G.REFERENCE_HSV_RANGES))
+
+
+def test_video_chain_4k_noisy_frames_vs_oracle(D):
+    """Config 5 on camera-like frames (bench.py --frame-noise): ±2 LSB of
+    noise on background and blob, so no 64-pixel slot is one colour and the
+    mask pass never takes its uniform-slot shortcut; bit-exact vs the oracle."""
+    from image_processor_pipeline_amd import geometry as G
+    from image_processor_pipeline_amd.video_chain import VideoChain, synthetic_frames
+    frames = synthetic_frames(2, 2160, 3840, 5, DEV, noise=2)
+    host = frames.cpu().numpy()
+    assert (host[:, :64, :64] != host[:, :1, :1]).any()   # the background is not flat
+    chain = VideoChain(2, 2160, 3840, DEV)
+    chain.run(frames)
+    res = chain.results()
+    for i in range(2):
+        exp = ops.keep_largest_component(ops.color_mask_bgra(host[i], G.REFERENCE_HSV_RANGES))
+        assert res[i] is not None and np.array_equal(res[i], exp), i
 
 
 def test_crop_to_bbox_and_vector_copy(D):

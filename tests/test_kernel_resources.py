@@ -37,14 +37,19 @@ def _asm(name: str, tmp_path: Path) -> Path:
 @pytest.mark.parametrize("name,hot", [("ipp_pipe", ("k_pipe_",)), ("ipp_ccl", ("k_ccl_",)),
                                       ("ipp_gather", ("k_rotate_flip_nearest", "k_copy_rows"))])
 def test_no_spills_no_scratch(name, hot, tmp_path):
-    ks = list(kernel_res.kernels(str(_asm(name, tmp_path))))
+    path = _asm(name, tmp_path)
+    ks = list(kernel_res.kernels(str(path)))
+    text = path.read_text()
     checked = 0
     for k in ks:
         if not any(h in k.get("name", "") for h in hot):
             continue
         checked += 1
         assert int(k.get("vgpr_spill_count", 0)) == 0, k["name"]
-        assert int(k.get("private_segment_fixed_size", 0)) == 0, k["name"]
+        # no scratch: none reserved, or (the backend can keep a frame for SGPR
+        # spill slots that all went to VGPR lanes) none ever accessed
+        if int(k.get("private_segment_fixed_size", 0)):
+            assert "scratch_" not in kernel_res.body(text, k["name"]), k["name"]
     assert checked > 0
 
 

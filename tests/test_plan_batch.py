@@ -224,3 +224,18 @@ def test_mfma_tile_matches_axis_planner(io, shift, phase, ident):
         nk = int(h4[1])
         assert np.array_equal(blk[:nk * 3072], blocks[hdr[t, 2] * 16:hdr[t, 2] * 16 + nk * 3072]), t
         assert h4[2] == t * int(ax["nkb"][0]) * 192
+
+
+def test_plan_rejects_overlays_wider_than_the_v_launch():
+    """Overlays wider than IPP_PIPE_MAX_OV_W are refused by the planner,
+    before ipp_pipe_hpass_bgcopy could write part of the composites (round-5
+    advisor finding); one just inside the limit plans."""
+    from image_processor_pipeline_amd import fused
+    from image_processor_pipeline_amd import _native as N
+    # a 4096² background at ratio 0.30: overlays of ≈ 1229 px
+    cfg = fused.PipeConfig(scale_min=0.30, scale_max=0.30)
+    with pytest.raises(ValueError, match="overlay width"):
+        fused.plan_pipe((256, 256), 4, (4096, 4096), 1, cfg, seed=3)
+    cfg = fused.PipeConfig(scale_min=0.15, scale_max=0.15)   # ≈ 614 px
+    plan = fused.plan_pipe((256, 256), 4, (4096, 4096), 1, cfg, seed=3)
+    assert plan.max_ov_w <= N.IPP_PIPE_MAX_OV_W

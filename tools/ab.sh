@@ -6,6 +6,6 @@ mkdir -p gpurun_out
 for spec in "$@"; do
   name=${spec%%:*}; envs=""; [ "$spec" != "$name" ] && envs=${spec#*:}
   lib=$PWD/image_processor_pipeline_amd/libipp.so; [ "$name" != base ] && lib=$PWD/variants/${name%%+*}/libipp.so
-  out=$(env $(echo $envs | tr ',' ' ') IPP_LIB_PATH=$lib timeout -k 10 300 python bench.py $ARGS --no-cpu-baseline --no-copy-ceiling --no-stream 2>gpurun_out/ab_err_${name}.log | tail -1)
+  out=$(env $(echo $envs | tr ',' ' ') IPP_AB_EXPERIMENT=1 IPP_LIB_PATH=$lib timeout -k 10 300 python bench.py $ARGS --no-cpu-baseline --no-copy-ceiling --no-stream 2>gpurun_out/ab_err_${name}.log | tail -1)
   echo "$spec $(echo "$out" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["kernels_ms"])')"
 done

@@ -13,7 +13,7 @@ for a in "$@"; do
   lib=""; args="$a"; envs=""
   case "$a" in *"|"*) lib="${a%%|*}"; args="${a#*|}";; esac
   case "$lib" in *"@"*) envs="${lib#*@}"; lib="${lib%%@*}";; esac
-  if [ -n "$lib" ]; then export IPP_LIB_PATH=$lib; else unset IPP_LIB_PATH; fi
+  if [ -n "$lib" ]; then export IPP_LIB_PATH=$lib IPP_AB_EXPERIMENT=1; else unset IPP_LIB_PATH IPP_AB_EXPERIMENT; fi
   timeout -k 10 300 env ${envs//,/ } python bench.py --no-cpu-baseline $args > gpurun_out/bench_${TAG}_$i.json.log 2>&1 || { tail -20 gpurun_out/bench_${TAG}_$i.json.log; exit 22; }
   python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'], d['value'], d['kernels_ms'])" gpurun_out/bench_${TAG}_$i.json.log "$a"
   i=$((i+1))

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 FILTER='k_pipe_hpass'
 for name in "$@"; do
   lib=$PWD/image_processor_pipeline_amd/libipp.so; [ "$name" != base ] && lib=$PWD/variants/$name/libipp.so
-  export IPP_LIB_PATH=$lib
+  export IPP_LIB_PATH=$lib IPP_AB_EXPERIMENT=1
   OUT=gpurun_out/$TAG/$name; mkdir -p $OUT
   i=0
   for grp in "TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum GRBM_GUI_ACTIVE TD_TD_BUSY_sum TD_TC_STALL_sum" \

@@ -13,6 +13,12 @@ def kernels(path):
         yield f
 
 
+def body(asm: str, name: str) -> str:
+    """The emitted ISA of kernel `name` (its label to its .Lfunc_end)."""
+    a = asm.index("\n" + name + ":")
+    return asm[a:asm.index(".Lfunc_end", a)]
+
+
 def main():
     path = sys.argv[1]
     flt = sys.argv[2] if len(sys.argv) > 2 else ""
@@ -23,6 +29,8 @@ def main():
         d = re.sub(r"\(anonymous namespace\)::", "", d)
         d = d.split("(")[0]
         if flt and flt not in d:
+            continue
+        if r.get("vgpr_count") is None:
             continue
         print(f"{d:60s} vgpr {r.get('vgpr_count'):>4} agpr {r.get('agpr_count', '0'):>3} sgpr {r.get('sgpr_count'):>4} "
               f"vspill {r.get('vgpr_spill_count'):>3} sspill {r.get('sgpr_spill_count'):>3} "
