@@ -1016,6 +1016,9 @@ k_ccl_inwords(const ipp_image_desc* __restrict__ descs, const ipp_ccl_work* __re
 }
 
 constexpr int CROP_BLOCKS = 256;  // blocks per image striding over the crop
+#ifndef IPP_CCL_CROP_ROWS
+#define IPP_CCL_CROP_ROWS 1  // the crop-fit by row waves (k_ccl_crop_rows); 0: the item stream (A/B)
+#endif
 
 __global__ void __launch_bounds__(256)
 k_ccl_crop_stream(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
@@ -1092,6 +1095,125 @@ k_ccl_crop_stream(const uint8_t* __restrict__ img, const ipp_image_desc* __restr
         if (it + stride < items) item(it + stride, ob, nb, qb);
         put(oa, na, qa);
         if (nb) put(ob, nb, qb);
+    }
+}
+
+// (b') k_ccl_crop_rows: the same crop-fit, one wave per crop row at a time.
+//     The stream above is texture-path bound (TA busy 96 % of the launch,
+//     profiles/r05/r05s9/prof_video4k): three unaligned dword loads plus the
+//     mask-word loads per 4 pixels.  Here a wave loads its row's source span
+//     with aligned 16-byte buffer loads (1 KB per instruction), stages it in
+//     LDS, and every lane assembles its 4 pixels from there (two LDS reads and
+//     v_alignbyte; the row's alignment is uniform), with the row's mask words
+//     read once into LDS too: per 4 pixels 0.75 load and 1 store instruction
+//     instead of ≈ 4.5 loads and 1 store.
+#ifndef IPP_CCL_CROP_ROW_BLOCKS
+#define IPP_CCL_CROP_ROW_BLOCKS 256
+#endif
+constexpr int CROP_ROW_BLOCKS = IPP_CCL_CROP_ROW_BLOCKS;  // blocks per image (4 waves each) striding over the crop rows
+constexpr int CROP_SEG = 4 * 256;            // output pixels per wave iteration (4 × 64 lanes × 4)
+constexpr int CROP_CHUNKS = 3 * CROP_SEG / 16 + 1;  // 16-B source chunks one iteration may touch
+
+struct CropRowsLds {
+    uint32_t stage[WAVES][CROP_CHUNKS * 4];  // source span of the wave's iteration
+    u64 words[WAVES][TW + 2];               // the row's mask words (tile columns tc0 ..), zero-padded
+};
+
+__global__ void __launch_bounds__(256)
+k_ccl_crop_rows(const uint8_t* __restrict__ img, const ipp_image_desc* __restrict__ descs,
+                const ipp_ccl_work* __restrict__ works, uint8_t* __restrict__ scratch,
+                int32_t* __restrict__ bbox, uint8_t* __restrict__ out,
+                const ipp_image_desc* __restrict__ out_descs) {
+    __shared__ CropRowsLds L;
+    const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int im = b / CROP_ROW_BLOCKS;
+    const int rb = b - im * CROP_ROW_BLOCKS;
+    const int bx0 = bbox[4 * im + 0], by0 = bbox[4 * im + 1], bx1 = bbox[4 * im + 2], by1 = bbox[4 * im + 3];
+    if (bx1 <= bx0 || by1 <= by0) {  // no kept component (k_ccl_finish folded in, as in k_ccl_crop_stream)
+        if (rb == 0 && threadIdx.x < 4) bbox[4 * im + threadIdx.x] = -1;
+        return;
+    }
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const ipp_image_desc d = descs[im];
+    const ipp_image_desc od = out_descs[im];
+    const Frame f = frame_of(d);
+    const Work k = work_of(scratch, works[im]);
+    const int cw = bx1 - bx0;
+    const int tc0 = bx0 >> 6, ntc = ((bx1 - 1) >> 6) - tc0 + 1;  // ≤ 61 tile columns
+    // The buffer starts at the 16-B aligned address at or below the frame
+    // (fmis bytes before it, in the same aligned chunk) and ends with the
+    // 4-aligned dword holding the frame's last byte: the range check works per
+    // dword (a straddling one reads 0), and neither extension crosses a page.
+    const uint8_t* fbase = img + d.off;
+    const uint32_t fmis = (uint32_t)(reinterpret_cast<uintptr_t>(fbase) & 15u);
+    const uint32_t fbytes = (uint32_t)((int64_t)d.h * d.pitch);
+    const uint32_t nrec = (fmis + fbytes + 3u) & ~3u;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(fbase - fmis), (short)0, (int)nrec, 0x00020000);
+    uint32_t* stage = L.stage[wave];
+    u64* words = L.words[wave];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    for (int y = by0 + rb * WAVES + wave; y < by1; y += CROP_ROW_BLOCKS * WAVES) {
+        // the row's kept-component words (lanes past the row's tiles: zero)
+        words[lane] = lane < ntc ? k.mask[((int64_t)(y >> 6) * f.tiles_x + tc0 + lane) * TH + (y & (TH - 1))] : 0ull;
+        if (lane < 2) words[TW + lane] = 0ull;
+        // buffer byte R of the row's first crop pixel; its 16-B chunk starts
+        // sh0 bytes before it
+        const uint32_t R = fmis + (uint32_t)y * (uint32_t)d.pitch + 3u * (uint32_t)bx0;
+        const uint32_t sh0 = R & 15u;
+        uint8_t* orow = out + od.off + (int64_t)(y - by0) * od.pitch;
+        for (int seg = 0; seg < cw; seg += CROP_SEG) {
+            const int npx = min(CROP_SEG, cw - seg);
+            // chunks [c0, c1) relative to the aligned start of the row
+            const int c0 = (int)((sh0 + 3u * (uint32_t)seg) >> 4);
+            const int c1 = (int)((sh0 + 3u * (uint32_t)(seg + npx) + 15u) >> 4);
+            u32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int c = c0 + lane + 64 * u;
+                if (c < c1) v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, R - sh0 + 16u * (uint32_t)c, 0, 0));
+            }
+            wave_sync();  // (the previous iteration's stage reads done)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int c = c0 + lane + 64 * u;
+                if (c < c1) *reinterpret_cast<u32x4*>(stage + 4 * (c - c0)) = v[u];
+            }
+            wave_sync();
+            // byte offset of pixel seg in the stage, and the row's dword alignment
+            const uint32_t o0 = sh0 + 3u * (uint32_t)seg - 16u * (uint32_t)c0;
+            const uint32_t sh = o0 & 3u;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int ox = seg + 256 * u + 4 * lane;
+                if (ox >= cw) continue;
+                const uint32_t o = o0 + 3u * (uint32_t)(ox - seg);   // ≡ sh (mod 4)
+                const uint32_t* q = stage + (o >> 2);
+                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+                const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh),
+                               w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                const uint32_t px[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 3), __builtin_amdgcn_alignbyte(w2, w1, 2),
+                                        w2 >> 8};
+                // the 4 pixels' bits: columns x .. x + 3 of the row's words
+                const int x = bx0 + ox, t = (x >> 6) - tc0, bb = x & 63;
+                const u64 lo = words[t] >> bb, hi = bb ? words[t + 1] << (64 - bb) : 0ull;
+                const uint32_t fb = (uint32_t)(lo | hi);
+                uint32_t o4[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) o4[i] = (px[i] & 0x00FFFFFFu) | (((fb >> i) & 1u) ? 0xFF000000u : 0u);
+                uint32_t* qo = reinterpret_cast<uint32_t*>(orow) + ox;
+                const int n = min(4, cw - ox);
+                if (n == 4 && (reinterpret_cast<uintptr_t>(qo) & 15u) == 0u) {
+                    __builtin_nontemporal_store(u32x4{o4[0], o4[1], o4[2], o4[3]}, reinterpret_cast<u32x4*>(qo));
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (i < n) qo[i] = o4[i];
+                }
+            }
+        }
+        wave_sync();  // words of this row read before the next row's
     }
 }
 
@@ -1237,8 +1359,12 @@ extern "C" int ipp_video_keep_largest(const uint8_t* frames, const ipp_image_des
     if (rc != IPP_OK) return rc;
     hipLaunchKernelGGL(k_ccl_inwords, L.group_grid, dim3(64 * WAVES), 0, s, descs, works, scratch, bbox,
                        L.groups_per_img, L.groups_x);
-    hipLaunchKernelGGL(k_ccl_crop_stream, dim3((uint32_t)((int64_t)CROP_BLOCKS * n_images)), dim3(256), 0, s, frames,
-                       descs, works, scratch, bbox, out, out_descs);
+    if (IPP_CCL_CROP_ROWS)
+        hipLaunchKernelGGL(k_ccl_crop_rows, dim3((uint32_t)((int64_t)CROP_ROW_BLOCKS * n_images)), dim3(256), 0, s,
+                           frames, descs, works, scratch, bbox, out, out_descs);
+    else
+        hipLaunchKernelGGL(k_ccl_crop_stream, dim3((uint32_t)((int64_t)CROP_BLOCKS * n_images)), dim3(256), 0, s,
+                           frames, descs, works, scratch, bbox, out, out_descs);
     IPP_CHECK_LAUNCH();
     return IPP_OK;
 }
