@@ -1112,6 +1112,9 @@ k_ccl_crop_stream(const uint8_t* __restrict__ img, const ipp_image_desc* __restr
 #define IPP_CCL_CROP_ROW_BLOCKS 256
 #endif
 constexpr int CROP_ROW_BLOCKS = IPP_CCL_CROP_ROW_BLOCKS;  // blocks per image (4 waves each) striding over the crop rows
+#ifndef IPP_CCL_CROP_PF
+#define IPP_CCL_CROP_PF 1  // the next (row, segment)'s loads in flight during this one (0: after it, A/B)
+#endif
 constexpr int CROP_SEG = 4 * 256;            // output pixels per wave iteration (4 × 64 lanes × 4)
 constexpr int CROP_CHUNKS = 3 * CROP_SEG / 16 + 1;  // 16-B source chunks one iteration may touch
 
@@ -1155,69 +1158,100 @@ k_ccl_crop_rows(const uint8_t* __restrict__ img, const ipp_image_desc* __restric
     uint32_t* stage = L.stage[wave];
     u64* words = L.words[wave];
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    for (int y = by0 + rb * WAVES + wave; y < by1; y += CROP_ROW_BLOCKS * WAVES) {
+    // The wave's (row, segment) units in order; each unit's chunk loads (and,
+    // on a row's first segment, its mask words) are issued before the
+    // previous unit is assembled and stored (IPP_CCL_CROP_PF), so their
+    // latency overlaps that work instead of stalling the wave.
+    struct Unit {
+        int y, seg;
+        uint32_t R, sh0;  // buffer byte of the row's first crop pixel; its offset in its 16-B chunk
+        int c0, c1;       // the segment's chunks
+    };
+    const int ystep = CROP_ROW_BLOCKS * WAVES;
+    auto unit_at = [&](int y, int seg) {
+        Unit u;
+        u.y = y;
+        u.seg = seg;
+        u.R = fmis + (uint32_t)y * (uint32_t)d.pitch + 3u * (uint32_t)bx0;
+        u.sh0 = u.R & 15u;
+        const int npx = min(CROP_SEG, cw - seg);
+        u.c0 = (int)((u.sh0 + 3u * (uint32_t)seg) >> 4);
+        u.c1 = (int)((u.sh0 + 3u * (uint32_t)(seg + npx) + 15u) >> 4);
+        return u;
+    };
+    auto next = [&](const Unit& u) { return u.seg + CROP_SEG < cw ? unit_at(u.y, u.seg + CROP_SEG) : unit_at(u.y + ystep, 0); };
+    auto load = [&](const Unit& u, u32x4 (&v)[4], u64& wd) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = u.c0 + lane + 64 * i;
+            if (c < u.c1)
+                v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, u.R - u.sh0 + 16u * (uint32_t)c, 0, 0));
+        }
         // the row's kept-component words, restricted by k_ccl_inwords (lanes
-        // past the row's tiles: zero).  (Restricting the one-component tiles
-        // here from their tile records instead, so that k_ccl_inwords skips
-        // them, measured ±0: 2.80 vs 2.81 ms, round 6.)
-        words[lane] = lane < ntc ? k.mask[((int64_t)(y >> 6) * f.tiles_x + tc0 + lane) * TH + (y & (TH - 1))] : 0ull;
-        if (lane < 2) words[TW + lane] = 0ull;
-        // buffer byte R of the row's first crop pixel; its 16-B chunk starts
-        // sh0 bytes before it
-        const uint32_t R = fmis + (uint32_t)y * (uint32_t)d.pitch + 3u * (uint32_t)bx0;
-        const uint32_t sh0 = R & 15u;
-        uint8_t* orow = out + od.off + (int64_t)(y - by0) * od.pitch;
-        for (int seg = 0; seg < cw; seg += CROP_SEG) {
-            const int npx = min(CROP_SEG, cw - seg);
-            // chunks [c0, c1) relative to the aligned start of the row
-            const int c0 = (int)((sh0 + 3u * (uint32_t)seg) >> 4);
-            const int c1 = (int)((sh0 + 3u * (uint32_t)(seg + npx) + 15u) >> 4);
-            u32x4 v[4];
+        // past the row's tiles: zero), on its first segment
+        if (u.seg == 0)
+            wd = lane < ntc ? k.mask[((int64_t)(u.y >> 6) * f.tiles_x + tc0 + lane) * TH + (u.y & (TH - 1))] : 0ull;
+    };
+    Unit cur = unit_at(by0 + rb * WAVES + wave, 0);
+    if (cur.y >= by1) return;
+    u32x4 vc[4];
+    u64 wc = 0ull;
+    load(cur, vc, wc);
+    for (;;) {
+        const Unit nx = next(cur);
+        const bool more = nx.y < by1;
+        u32x4 vn[4];
+        u64 wn = 0ull;
+        if (IPP_CCL_CROP_PF && more) load(nx, vn, wn);
+        wave_sync();  // (the previous unit's stage and word reads done)
+        if (cur.seg == 0) {
+            words[lane] = wc;
+            if (lane < 2) words[TW + lane] = 0ull;
+        }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int c = c0 + lane + 64 * u;
-                if (c < c1) v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, R - sh0 + 16u * (uint32_t)c, 0, 0));
-            }
-            wave_sync();  // (the previous iteration's stage reads done)
+        for (int i = 0; i < 4; ++i) {
+            const int c = cur.c0 + lane + 64 * i;
+            if (c < cur.c1) *reinterpret_cast<u32x4*>(stage + 4 * (c - cur.c0)) = vc[i];
+        }
+        wave_sync();
+        uint8_t* orow = out + od.off + (int64_t)(cur.y - by0) * od.pitch;
+        // byte offset of pixel seg in the stage, and the row's dword alignment
+        const uint32_t o0 = cur.sh0 + 3u * (uint32_t)cur.seg - 16u * (uint32_t)cur.c0;
+        const uint32_t sh = o0 & 3u;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int c = c0 + lane + 64 * u;
-                if (c < c1) *reinterpret_cast<u32x4*>(stage + 4 * (c - c0)) = v[u];
-            }
-            wave_sync();
-            // byte offset of pixel seg in the stage, and the row's dword alignment
-            const uint32_t o0 = sh0 + 3u * (uint32_t)seg - 16u * (uint32_t)c0;
-            const uint32_t sh = o0 & 3u;
+        for (int u = 0; u < 4; ++u) {
+            const int ox = cur.seg + 256 * u + 4 * lane;
+            if (ox >= cw) continue;
+            const uint32_t o = o0 + 3u * (uint32_t)(ox - cur.seg);  // ≡ sh (mod 4)
+            const uint32_t* q = stage + (o >> 2);
+            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh),
+                           w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+            const uint32_t px[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 3), __builtin_amdgcn_alignbyte(w2, w1, 2),
+                                    w2 >> 8};
+            // the 4 pixels' bits: columns x .. x + 3 of the row's words
+            const int x = bx0 + ox, t = (x >> 6) - tc0, bb = x & 63;
+            const u64 lo = words[t] >> bb, hi = bb ? words[t + 1] << (64 - bb) : 0ull;
+            const uint32_t fb = (uint32_t)(lo | hi);
+            uint32_t o4[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int ox = seg + 256 * u + 4 * lane;
-                if (ox >= cw) continue;
-                const uint32_t o = o0 + 3u * (uint32_t)(ox - seg);   // ≡ sh (mod 4)
-                const uint32_t* q = stage + (o >> 2);
-                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
-                const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh),
-                               w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-                const uint32_t px[4] = {w0, __builtin_amdgcn_alignbyte(w1, w0, 3), __builtin_amdgcn_alignbyte(w2, w1, 2),
-                                        w2 >> 8};
-                // the 4 pixels' bits: columns x .. x + 3 of the row's words
-                const int x = bx0 + ox, t = (x >> 6) - tc0, bb = x & 63;
-                const u64 lo = words[t] >> bb, hi = bb ? words[t + 1] << (64 - bb) : 0ull;
-                const uint32_t fb = (uint32_t)(lo | hi);
-                uint32_t o4[4];
+            for (int i = 0; i < 4; ++i) o4[i] = (px[i] & 0x00FFFFFFu) | (((fb >> i) & 1u) ? 0xFF000000u : 0u);
+            uint32_t* qo = reinterpret_cast<uint32_t*>(orow) + ox;
+            const int n = min(4, cw - ox);
+            if (n == 4 && (reinterpret_cast<uintptr_t>(qo) & 15u) == 0u) {
+                __builtin_nontemporal_store(u32x4{o4[0], o4[1], o4[2], o4[3]}, reinterpret_cast<u32x4*>(qo));
+            } else {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) o4[i] = (px[i] & 0x00FFFFFFu) | (((fb >> i) & 1u) ? 0xFF000000u : 0u);
-                uint32_t* qo = reinterpret_cast<uint32_t*>(orow) + ox;
-                const int n = min(4, cw - ox);
-                if (n == 4 && (reinterpret_cast<uintptr_t>(qo) & 15u) == 0u) {
-                    __builtin_nontemporal_store(u32x4{o4[0], o4[1], o4[2], o4[3]}, reinterpret_cast<u32x4*>(qo));
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (i < n) qo[i] = o4[i];
-                }
+                for (int i = 0; i < 4; ++i)
+                    if (i < n) qo[i] = o4[i];
             }
         }
-        wave_sync();  // words of this row read before the next row's
+        if (!more) break;
+        if (!IPP_CCL_CROP_PF) load(nx, vn, wn);
+        cur = nx;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vc[i] = vn[i];
+        if (cur.seg == 0) wc = wn;
     }
 }
 
