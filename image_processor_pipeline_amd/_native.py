@@ -47,6 +47,7 @@ GATHER_DESC = np.dtype([
     ("src_w", _I4), ("src_h", _I4), ("in_x0", _I4), ("in_y0", _I4), ("in_w", _I4), ("in_h", _I4),
     ("a0", _I4), ("a1", _I4), ("a2", _I4), ("a3", _I4), ("a4", _I4), ("a5", _I4),
     ("out_w", _I4), ("out_h", _I4), ("off_x", _I4), ("off_y", _I4), ("flip", _I4), ("dst_pitch", _I4),
+    ("base_off", _I8), ("lim", np.uint32), ("b", _I4, (6,)), ("prepared", _I4),
 ], align=True)
 
 AFFINE_DESC = np.dtype([
@@ -124,6 +125,7 @@ _L = ctypes.c_int64
 _D = ctypes.c_double
 SIGNATURES = {
     "ipp_rotate_flip_nearest": (_I, [_P, _P, _P, _I, _I, _I, _P]),
+    "ipp_gather_prepare": (_I, [_P, _I]),
     "ipp_rotate_bilinear": (_I, [_P, _P, _P, _I, _I, _I, _P]),
     "ipp_copy_window": (_I, [_P, _P, _P, _I, _I, _I, _P]),
     "ipp_crop_to_bbox": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P]),

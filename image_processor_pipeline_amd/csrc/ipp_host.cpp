@@ -185,6 +185,30 @@ extern "C" int ipp_plan_opaque_bbox(int32_t in_w, int32_t in_h, const int32_t a[
 
 extern "C" const char* ipp_version(void) { return "ipp 0.1.0 (gfx950)"; }
 
+// The gather sampler of ipp_sampler.h make_sampler, once per image on the
+// host (rotations.py:96 affine with symmetry.py:114-119's flip and the bbox
+// crop of :99-101 folded in; 32-bit wrap-around as in the kernels).
+extern "C" int ipp_gather_prepare(ipp_gather_desc* descs, int32_t n) {
+    if (n < 0 || (n > 0 && !descs)) return IPP_E_ARG;
+    for (int32_t i = 0; i < n; ++i) {
+        ipp_gather_desc& g = descs[i];
+        g.base_off = g.src_off + (int64_t)g.in_y0 * g.src_pitch + (int64_t)g.in_x0 * g.src_cn;
+        const int64_t avail = (int64_t)(g.src_h - g.in_y0) * g.src_pitch - (int64_t)g.in_x0 * g.src_cn;
+        g.lim = (uint32_t)(avail - 4);
+        const uint32_t sgx = (g.flip & 1) ? 0xFFFFFFFFu : 1u, sgy = (g.flip & 2) ? 0xFFFFFFFFu : 1u;
+        const uint32_t sx0 = (uint32_t)(g.off_x + ((g.flip & 1) ? g.out_w - 1 : 0));
+        const uint32_t sy0 = (uint32_t)(g.off_y + ((g.flip & 2) ? g.out_h - 1 : 0));
+        g.b[0] = (int32_t)(sgx * (uint32_t)g.a0);
+        g.b[1] = (int32_t)(sgy * (uint32_t)g.a1);
+        g.b[2] = (int32_t)((uint32_t)g.a2 + sy0 * (uint32_t)g.a1 + sx0 * (uint32_t)g.a0);
+        g.b[3] = (int32_t)(sgx * (uint32_t)g.a3);
+        g.b[4] = (int32_t)(sgy * (uint32_t)g.a4);
+        g.b[5] = (int32_t)((uint32_t)g.a5 + sy0 * (uint32_t)g.a4 + sx0 * (uint32_t)g.a3);
+        g.prepared = 1;
+    }
+    return IPP_OK;
+}
+
 // Balanced signed bytes of a 22-bit tap: k = b0 + 256 b1 + 65536 b2, each
 // b in [-128, 127] (the MFMA tile format below).
 namespace {

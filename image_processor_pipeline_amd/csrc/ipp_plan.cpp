@@ -592,6 +592,7 @@ extern "C" int ipp_plan_pipe_batch(const ipp_pipe_plan_cfg* cfg, ipp_pipe_item* 
         g.off_x = it.cut_x;
         g.off_y = it.cut_y;
         g.flip = c.sym_flip[it.sym];
+        ipp_gather_prepare(&g, 1);
         // T rows are grouped by 4; V tiles read up to 64·nK rows past their
         // 16-aligned start
         const int64_t groups = (((int64_t)(rows + 15) / 16) * 16 + 64 * nkb_v + 16) / 4;

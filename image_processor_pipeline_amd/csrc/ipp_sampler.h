@@ -14,8 +14,25 @@ struct Sampler {
     int32_t in_w, in_h;
 };
 
+#ifndef IPP_SAMPLER_PREPARED
+#define IPP_SAMPLER_PREPARED 1  // (0: A/B builds recompute the sampler per block)
+#endif
 __device__ __forceinline__ Sampler make_sampler(const uint8_t* src, const ipp_gather_desc& g) {
     Sampler s;
+    if (IPP_SAMPLER_PREPARED && g.prepared) {  // ipp_gather_prepare did the arithmetic below once per image (block-uniform)
+        s.base = src + g.base_off;
+        s.pitch = (uint32_t)g.src_pitch;
+        s.lim = g.lim;
+        s.b0 = g.b[0];
+        s.b1 = g.b[1];
+        s.b2 = g.b[2];
+        s.b3 = g.b[3];
+        s.b4 = g.b[4];
+        s.b5 = g.b[5];
+        s.in_w = g.in_w;
+        s.in_h = g.in_h;
+        return s;
+    }
     s.base = src + g.src_off + (int64_t)g.in_y0 * g.src_pitch + (int64_t)g.in_x0 * g.src_cn;
     s.pitch = (uint32_t)g.src_pitch;
     const int64_t avail = (int64_t)(g.src_h - g.in_y0) * g.src_pitch - (int64_t)g.in_x0 * g.src_cn;

@@ -101,6 +101,9 @@ def plan_rotate_flip(src_dims: Sequence[Tuple[int, int, int]], angles: Sequence[
         pitches[i] = pitch
         off += pitch * oh
         max_w, max_h = max(max_w, ow), max(max_h, oh)
+    # the per-image sampler (flip and bbox origin folded into the affine),
+    # once here instead of in every block of the kernel
+    N.check(N.load().ipp_gather_prepare(N.np_ptr(d), n), "ipp_gather_prepare")
     return GatherPlan(d, shapes, offs, pitches, off, max_w, max_h)
 
 

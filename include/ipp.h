@@ -61,7 +61,19 @@ typedef struct ipp_gather_desc {
     int32_t off_x, off_y;             /* bbox origin inside the canvas      */
     int32_t flip;                     /* bit0: mirror x ('h'), bit1: mirror y ('v') */
     int32_t dst_pitch;                /* bytes per output row (≥ 4*out_w)   */
+    /* The sampler of the fields above, filled by ipp_gather_prepare
+     * (prepared = 1) so that every block of the gather kernels reads it
+     * instead of recomputing it; with prepared = 0 the kernels compute it. */
+    int64_t base_off;                 /* src_off + in_y0*src_pitch + in_x0*src_cn */
+    uint32_t lim;                     /* last byte offset from base where a 4-byte load fits */
+    int32_t b[6];                     /* 16.16 map with the flip and bbox origin folded in:
+                                         x_src = b2 + y*b1 + x*b0, y_src = b5 + y*b4 + x*b3 */
+    int32_t prepared;
 } ipp_gather_desc;
+
+/* Fills the sampler fields of n host-side descriptors (same arithmetic as
+ * the kernels' own, 32-bit wrap-around). */
+int ipp_gather_prepare(ipp_gather_desc* descs, int32_t n);
 
 /* rotations.py:55 convert('RGBA') + :96 rotate(angle, expand=True) + :99-101
  * getbbox()/crop(), recadrages.py:46 margin crop, symmetry.py:114-119 flip —

@@ -75,6 +75,25 @@ def test_rotate_flip_batch_vs_oracle(D, shape):
         assert np.array_equal(got[i], exp), (i, angles[i], syms[i])
 
 
+def test_rotate_flip_unprepared_descriptors_match(D):
+    """Descriptors without the host-precomputed sampler (prepared = 0, the
+    kernel computes it per block) give the same bytes as prepared ones
+    (ipp_gather_prepare), margin windows and every flip included."""
+    rng = np.random.default_rng(9)
+    n, h, w = 8, 97, 131
+    src = rng.integers(0, 256, (n, h, w, 3), np.uint8)
+    angles = [float(a) for a in rng.uniform(-360, 360, n)]
+    flips = [i % 4 for i in range(n)]
+    wins = [(3 * i % 7, i % 5, w - 11, h - 9) for i in range(n)]
+    plan = D.plan_rotate_flip([(h, w, 3)] * n, angles, flips, windows=wins, src_offsets=[i * h * w * 3 for i in range(n)])
+    assert (plan.descs["prepared"] == 1).all()
+    a = D.rotate_flip_nearest(_t(src).reshape(-1), plan).cpu().numpy()
+    plan.descs["prepared"] = 0
+    plan.descs["b"] = 0          # (garbage the kernel must not read)
+    b = D.rotate_flip_nearest(_t(src).reshape(-1), plan).cpu().numpy()
+    assert np.array_equal(a, b)
+
+
 def test_rotate_with_margin_window(D):
     rng = np.random.default_rng(2)
     h, w = 120, 90
