@@ -222,19 +222,30 @@ struct Hp2Chunk {
     int nsteps;   // this wave's phase-1 steps (16 groups per step over the block)
 };
 
+// The chunk's four candidate headers are read at once (scalar loads of 64
+// B; reading up to three headers past the table stays inside the tap buffer
+// — the tile biases follow it): per chunk one load round trip instead of a
+// chain of dependent ones.
 __device__ __forceinline__ Hp2Chunk hp2_chunk(const int4* hdr, int s0, int ntiles, int& filled, int wave) {
     Hp2Chunk c;
     c.s0 = s0;
-    const int W0 = hdr[s0].x;
-    int s1 = min(s0 + 4, ntiles), W1;
-    for (;;) {
-        W1 = W0;
-        for (int t = s0; t < s1; ++t) W1 = max(W1, hdr[t].x + 64 * hdr[t].y);
-        if (s1 - s0 == 1 || W1 - W0 <= RING) break;
-        --s1;
+    int4 hh[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hh[k] = hdr[s0 + k];
+    const int W0 = hh[0].x;
+    int W1 = hh[0].x + 64 * hh[0].y, s1 = s0 + 1;
+    if (W1 - W0 > RING && threadIdx.x == 0) atomicOr(&g_pipe_status, 1);  // single tile beyond the ring
+    bool grow = true;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+        const int e = max(W1, hh[k].x + 64 * hh[k].y);
+        grow = grow && s0 + k < ntiles && e - W0 <= RING;  // the longest prefix of ≤ 4 tiles that fits
+        if (grow) {
+            W1 = e;
+            s1 = s0 + k + 1;
+        }
     }
     c.s1 = s1;
-    if (W1 - W0 > RING && threadIdx.x == 0) atomicOr(&g_pipe_status, 1);  // single tile beyond the ring
     c.c0 = max(filled, W0);
     c.ng4 = max(0, (W1 - c.c0) >> 2);
     c.nsteps = c.ng4 > wave * 4 ? (c.ng4 - wave * 4 + 4 * HP_NW - 1) / (4 * HP_NW) : 0;
@@ -251,7 +262,7 @@ template <int NR, bool ZONES, int CN, bool CLAMP>
 __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win, int wave, const Hp2Block& B,
                                             uint8_t* __restrict__ tmp, const int32_t* __restrict__ coefs,
                                             const ipp_resample_desc& h, int row0, int nrows, const int32_t* zc0,
-                                            const int32_t* zcw, uint32_t zrow, uint32_t fill) {
+                                            const int32_t* zcw, uint32_t zrow) {
     const int lane = threadIdx.x & 63;
     const int r = 2 * (lane >> 3) + ((lane >> 1) & 1);  // the lane's window row
     const int ntiles = (h.out_len + 15) >> 4;
@@ -287,6 +298,11 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
     };
     issue(ck, 0, xxl, yyl, RA);
     issue(ck, 1, xxl + sx, yyl + sy, RB);
+    // The block's first gathers fly across the table barrier (r06k A/B:
+    // −0.01 ms per headline step).
+    __syncthreads();  // tables visible
+    // Fill value (raw 0): uniform over the block except for zone bits.
+    const uint32_t fill = __builtin_amdgcn_readfirstlane(hsv2_px<NR, ZONES>(T, 0u, ~0u));  // (in an SGPR)
 
     for (;;) {
         // This wave's tile taps for the first K step, in flight during phase 1.
@@ -367,8 +383,22 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // nsteps is dead).  With no early exit each set keeps its registers;
         // an exit mid-rotation made the compiler shuffle the sets through
         // copies, and copying a register whose load is in flight waits for it.
+        //
+        // The phase-2 column bias and (compact tiles) the lane's group meta
+        // are issued at the start of the last rotation: in flight during all
+        // of phase 1 they cost the registers phase 1 needs; issued after it,
+        // their latency sat exposed before the barrier (r06j/r06k A/B: −0.075
+        // ms per headline step).  (Reading the next chunk's headers there too
+        // spilled SGPRs to scratch.)  The gathers issued before them wait a
+        // little longer than needed (vmcnt counts the two loads as newer).
+        bool mb = false;
         for (int st = 0; st < nsteps; st += 3) {
             iss(st + 2, RC);
+            if (st + 3 >= nsteps) {
+                meta = reinterpret_cast<const int32_t*>(tblk + th.z)[lane & 15];
+                bias = tbias[min(16 * te + (lane & 15), h.out_len - 1)];
+                mb = true;
+            }
             process(RA, st, 4 * (RB.live + RC.live));
             iss(st + 3, RA);
             process(RB, st + 1, 4 * (RC.live + RA.live));
@@ -380,12 +410,10 @@ __device__ __forceinline__ void hpass2_body(const HsvTables<NR>& T, WinRing& win
         // and meta loads below are waited for on every path before the next
         // chunk's gathers: a compiler wait for them after those asm gathers
         // would drain the gathers as well.
-        // The phase-2 column bias and (compact tiles) the lane's group meta,
-        // loaded only now: in flight during phase 1 they cost the registers
-        // that phase 1 needs.  Their latency overlaps the next chunk's header
-        // reads below.
-        meta = reinterpret_cast<const int32_t*>(tblk + th.z)[lane & 15];
-        bias = tbias[min(16 * te + (lane & 15), h.out_len - 1)];
+        if (!mb) {  // (a wave with no phase-1 steps)
+            meta = reinterpret_cast<const int32_t*>(tblk + th.z)[lane & 15];
+            bias = tbias[min(16 * te + (lane & 15), h.out_len - 1)];
+        }
         const int s1 = ck.s1;
         const bool more = s1 < ntiles;
         if (more) {
@@ -830,14 +858,12 @@ __device__ __forceinline__ void hpass_block(Hpass2Lds<NR>& L, const uint8_t* __r
         B.xhi = bhi;
     }
 
-    __syncthreads();  // tables visible
-    // Fill value (raw 0): uniform over the block except for zone bits.
-    const uint32_t fill = __builtin_amdgcn_readfirstlane(hsv2_px<NR, ZONES>(L.T, 0u, ~0u));  // (in an SGPR)
+    // (the table barrier is in the body, after the first gathers)
     const int nrows = min(HR, h.lines - row0);
     if (fast)
-        hpass2_body<NR, ZONES, CN, false>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+        hpass2_body<NR, ZONES, CN, false>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow);
     else
-        hpass2_body<NR, ZONES, CN, true>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow, fill);
+        hpass2_body<NR, ZONES, CN, true>(L.T, L.win, wave, B, tmp, coefs, h, row0, nrows, zc0, zcw, zrow);
 }
 
 // 4 waves per SIMD (≤ 128 VGPRs); the zone forms get 3 (their per-lane zone
