@@ -34,7 +34,14 @@ struct TileGrid {
 //   ROWS:  wave w covers rows 4w..4w+3 directly (16 lanes × 4 pixels per row).
 // Tiles per block: 1 / 2 / 4 measured 2.87 / 2.84 / 3.07 ms for config 2
 // (round 4, nontemporal stores).
-constexpr int RT = 2;  // tiles per block (rows of 16)
+// Tiles per block 2 / 3 / 4 / 5: 2.44 / 2.41 / 2.42 / 2.45 ms for config 2
+// (round 6, one box, profiles/r06/ab_rotflip_rt_r06o.txt).  A map without
+// the LDS restage — wave w the 8 rows × 32 columns at (8(w>>1), 32(w&1)),
+// 4 adjacent pixels per lane stored directly — measured 2.52 (r06n).
+#ifndef IPP_ROT_RT
+#define IPP_ROT_RT 3
+#endif
+constexpr int RT = IPP_ROT_RT;  // tiles per block (rows of 16)
 
 template <int CN, bool PATCH, bool DENSE = false>
 __device__ __forceinline__ void rotate_tiles(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
