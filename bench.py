@@ -74,6 +74,11 @@ def parse(argv=None):
                     help="--stream: launch the pipe on the default-priority stream (not a high-priority one)")
     ap.add_argument("--stream-lookahead", type=int, default=2,
                     help="--stream: batches planned ahead of the running one (worker threads, side streams)")
+    ap.add_argument("--pipe-parts", type=int, default=1,
+                    help="pipe5: run the batch as N item ranges, each range's V launch on a side stream "
+                         "overlapping the next range's H launch (1 = the two launches back to back)")
+    ap.add_argument("--pipe-ratio", type=float, default=1.0,
+                    help="pipe5 with --pipe-parts: item range k holds a share proportional to ratio**k")
     ap.add_argument("--no-legs", action="store_true",
                     help="pipe5: skip the config-2 (rotflip) and config-5 (video4k) legs that the default run "
                          "times after the headline and reports under 'workloads'")
@@ -370,6 +375,10 @@ def run_workload(args, rank, world, dev):
             bg_copy = {"bg_bytes_loaded": int(plan.copy_read_bytes), "items_per_group": _native.IPP_PIPE_COPY_GROUP}
             launches = [("ipp_pipe_hpass_bgcopy", lambda: runner.hpass_bgcopy(src, bgs, out)),
                         ("ipp_pipe_vblend_bands", lambda: runner.vblend_bands(bgs, out))]
+            if args.pipe_parts > 1:
+                launches = [("ipp_pipe_overlapped", lambda: runner.run_overlapped(src, bgs, out, args.pipe_parts,
+                                                                                     args.pipe_ratio))]
+                algo = {"ipp_pipe_overlapped": sum(algo.values())}
         outputs = lambda: {start + i: _digest(out[i].cpu().numpy()) for i in range(B)}
         workload = "5-stage pipe: crop(64px)->rotate(NEAREST,expand,bbox)->flip->HSV mask(4 ref ranges)->LANCZOS+paste"
     elif args.workload == "video4k":

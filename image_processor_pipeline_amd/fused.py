@@ -329,6 +329,41 @@ class PipeRunner:
                                                n, p.bg_w, p.bg_h, p.max_ov_w, p.max_ov_h, p.tap_format,
                                                _stream(self.device)), "ipp_pipe_vblend_bands")
 
+    def run_overlapped(self, src: torch.Tensor, bgs: torch.Tensor, out: torch.Tensor, parts: int,
+                       ratio: float = 1.0) -> None:
+        """The batch in `parts` consecutive item ranges: the H launch of range k+1
+        runs on the caller's stream while the V launch of range k runs on a
+        side stream (event-ordered after its own H launch), so the V pass's
+        HBM streaming overlaps the texture-bound H pass.  The ranges are whole
+        copy groups of the H launch; the caller's stream waits for the last V
+        launch."""
+        p = self.plan
+        n = len(p.descs)
+        g = N.IPP_PIPE_COPY_GROUP
+        groups = (n + g - 1) // g
+        w = [ratio ** k for k in range(parts)]
+        cum = [sum(w[:k]) / sum(w) for k in range(parts + 1)]
+        bounds = [min(n, g * int(round(groups * c))) for c in cum]
+        main = torch.cuda.current_stream(self.device)
+        if getattr(self, "_vstream", None) is None:
+            self._vstream = torch.cuda.Stream(self.device)
+            self._events = []
+        side = self._vstream
+        while len(self._events) < parts:
+            self._events.append(torch.cuda.Event())
+        side.wait_stream(main)  # inputs and tmp reuse ordered after the caller's work
+        for k in range(parts):
+            i0, i1 = bounds[k], bounds[k + 1]
+            if i1 <= i0:
+                continue
+            self.hpass_bgcopy(src, bgs, out, items=(i0, i1 - i0))
+            ev = self._events[k]
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                self.vblend_bands(bgs, out, items=(i0, i1 - i0))
+        main.wait_stream(side)
+
     def status(self) -> int:
         """Sticky status of the pipe kernels since the last call (ipp_pipe_status;
         bit 0: an H tile's window exceeded the LDS ring).  Synchronises."""
