@@ -229,3 +229,24 @@ def test_crop_square_non_square_vs_restatement(tmp_path, hw, lines):
         exp_img, exp_txt = _crop_square_restated(img, lines, random.Random(seed))
         assert np.array_equal(ipp_io.imread(res[0]), exp_img), seed
         assert res[1].read_text() == exp_txt, seed
+
+
+@pytest.mark.parametrize("parts,ratio", [(3, 1.0), (2, 0.3), (5, 1.0)])
+def test_overlapped_item_ranges_equal_sequential(parts, ratio):
+    """PipeRunner.run_overlapped (bench.py --pipe-parts): V launches of item
+    range k on a side stream beside range k+1's H launch give the same bytes
+    as the two whole-batch launches, including ranges that end mid-batch and
+    empty ranges (more parts than copy groups)."""
+    from image_processor_pipeline_amd import fused
+    n, S, K = 21, 256, 3
+    g = torch.Generator().manual_seed(5)
+    src = torch.randint(0, 256, (n, S, S, 3), dtype=torch.uint8, generator=g).to(DEV)
+    bgs = torch.randint(0, 256, (K, S, S, 3), dtype=torch.uint8, generator=g).to(DEV)
+    plan = fused.plan_pipe((S, S), n, (S, S), K, fused.PipeConfig(), seed=11)
+    runner = fused.PipeRunner(plan, DEV)
+    ref = torch.zeros((n, S, S, 3), dtype=torch.uint8, device=DEV)
+    runner.run(src, bgs, ref)
+    out = torch.full((n, S, S, 3), 7, dtype=torch.uint8, device=DEV)
+    runner.run_overlapped(src, bgs, out, parts, ratio)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
