@@ -299,6 +299,20 @@ def plan_taps(plan: PipePlan, device, stream=None) -> Tuple[torch.Tensor, int]:
     return coefs, int(stats[0])
 
 
+def overlap_bounds(n: int, parts: int, ratio: float = 1.0, group: int = N.IPP_PIPE_COPY_GROUP) -> List[int]:
+    """Item-range bounds of PipeRunner.run_overlapped: `parts` ranges of whole
+    copy groups, range k holding a share proportional to ratio**k; bounds[0]
+    = 0, bounds[-1] = n, non-decreasing (a range may be empty)."""
+    if n < 0 or parts < 1 or ratio <= 0:
+        raise ValueError(f"overlap_bounds: n={n} parts={parts} ratio={ratio}")
+    groups = (n + group - 1) // group
+    w = [ratio ** k for k in range(parts)]
+    cum = [sum(w[:k]) / sum(w) for k in range(parts + 1)]
+    b = [min(n, group * int(round(groups * c))) for c in cum]
+    b[-1] = n
+    return b
+
+
 class PipeRunner:
     """Device-resident plan + scratch for repeated runs of one batch."""
 
@@ -337,13 +351,7 @@ class PipeRunner:
         HBM streaming overlaps the texture-bound H pass.  The ranges are whole
         copy groups of the H launch; the caller's stream waits for the last V
         launch."""
-        p = self.plan
-        n = len(p.descs)
-        g = N.IPP_PIPE_COPY_GROUP
-        groups = (n + g - 1) // g
-        w = [ratio ** k for k in range(parts)]
-        cum = [sum(w[:k]) / sum(w) for k in range(parts + 1)]
-        bounds = [min(n, g * int(round(groups * c))) for c in cum]
+        bounds = overlap_bounds(len(self.plan.descs), parts, ratio)
         main = torch.cuda.current_stream(self.device)
         if getattr(self, "_vstream", None) is None:
             self._vstream = torch.cuda.Stream(self.device)
